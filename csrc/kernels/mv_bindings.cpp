@@ -1,0 +1,251 @@
+// PyTorch bindings for the mivod gfx950 kernels (module mivod._mvk).
+// Every entry point validates shapes / dtypes / devices on the host before a
+// launch: a kernel is never started on operands that disagree with the grid
+// it assumes.  All launches go to the caller's current HIP stream.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+
+#include <vector>
+
+#include "mv_kernels.h"
+
+namespace {
+
+constexpr int64_t kChunk = 4096;
+
+int dtype_code(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    default: TORCH_CHECK(false, "mivod kernels: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+void check_dev(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda(), "mivod kernels: ", what, " must be a GPU tensor");
+  TORCH_CHECK(t.is_non_overlapping_and_dense(), "mivod kernels: ", what,
+              " must be dense and non-overlapping");
+}
+
+void check_flat(const at::Tensor& t, const char* what) {
+  check_dev(t, what);
+  TORCH_CHECK(t.is_contiguous(), "mivod kernels: ", what, " must be contiguous");
+}
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+int* nf_ptr(const c10::optional<at::Tensor>& nf) {
+  if (!nf.has_value()) return nullptr;
+  TORCH_CHECK(nf->is_cuda() && nf->scalar_type() == at::kInt && nf->numel() >= 1,
+              "nonfinite flag must be an int32 GPU tensor");
+  return nf->data_ptr<int>();
+}
+
+// K1/K2: pack (to_flat) or unpack tensors <-> flat[offsets[i] : offsets[i]+numel]
+void mt_copy(const std::vector<at::Tensor>& tensors, at::Tensor flat,
+             const std::vector<int64_t>& offsets, bool to_flat, double scale,
+             c10::optional<at::Tensor> nonfinite) {
+  TORCH_CHECK(tensors.size() == offsets.size(), "mt_copy: tensors/offsets length mismatch");
+  if (tensors.empty()) return;
+  check_flat(flat, "flat");
+  c10::DeviceGuard guard(flat.device());
+  const int tdt = dtype_code(tensors[0]);
+  const int fdt = dtype_code(flat);
+  const int64_t fnumel = flat.numel();
+  int* nf = nf_ptr(nonfinite);
+  hipStream_t st = cur_stream();
+  MtArgs a;
+  a.ntensors = 0;
+  a.chunk_start[0] = 0;
+  auto flush = [&]() {
+    if (a.ntensors == 0) return;
+    mv_launch_mt_copy(a, tdt, flat.data_ptr(), fdt, to_flat, (float)scale, nf, st);
+    a.ntensors = 0;
+    a.chunk_start[0] = 0;
+  };
+  for (size_t i = 0; i < tensors.size(); ++i) {
+    const at::Tensor& t = tensors[i];
+    check_dev(t, "tensor");
+    TORCH_CHECK(t.device() == flat.device(), "mt_copy: tensor on a different device");
+    TORCH_CHECK(dtype_code(t) == tdt, "mt_copy: mixed tensor dtypes in one call");
+    const int64_t n = t.numel();
+    TORCH_CHECK(offsets[i] >= 0 && offsets[i] + n <= fnumel, "mt_copy: tensor ", i,
+                " [", offsets[i], ", +", n, ") exceeds flat buffer of ", fnumel);
+    if (n == 0) continue;
+    const int64_t chunks = (n + kChunk - 1) / kChunk;
+    TORCH_CHECK(chunks < (1 << 30), "mt_copy: tensor too large");
+    if (a.ntensors == kMvMaxTensors ||
+        (int64_t)a.chunk_start[a.ntensors] + chunks > (int64_t)(1u << 30))
+      flush();
+    const int k = a.ntensors++;
+    a.ptr[k] = t.data_ptr();
+    a.numel[k] = n;
+    a.flat_off[k] = offsets[i];
+    a.chunk_start[k + 1] = a.chunk_start[k] + (int32_t)chunks;
+  }
+  flush();
+}
+
+void flat_cast(at::Tensor src, at::Tensor dst, double scale, c10::optional<at::Tensor> nonfinite) {
+  check_flat(src, "src");
+  check_flat(dst, "dst");
+  TORCH_CHECK(src.numel() == dst.numel(), "flat_cast: numel mismatch");
+  c10::DeviceGuard guard(src.device());
+  mv_launch_flat_cast(src.data_ptr(), dtype_code(src), dst.data_ptr(), dtype_code(dst), src.numel(),
+                      (float)scale, nf_ptr(nonfinite), cur_stream());
+}
+
+void check_master(const at::Tensor& g, const at::Tensor& t, const char* what) {
+  check_flat(t, what);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, what, " must be fp32");
+  TORCH_CHECK(t.numel() == g.numel(), what, " numel ", t.numel(), " != grad numel ", g.numel());
+  TORCH_CHECK(t.device() == g.device(), what, " on a different device");
+}
+
+void* model_ptr(const c10::optional<at::Tensor>& model, const at::Tensor& g, int* md) {
+  *md = 0;
+  if (!model.has_value()) return nullptr;
+  check_flat(*model, "model");
+  TORCH_CHECK(model->numel() == g.numel(), "model numel mismatch");
+  *md = dtype_code(*model);
+  return model->data_ptr();
+}
+
+void sgd_step(at::Tensor g, at::Tensor w, c10::optional<at::Tensor> mom,
+              c10::optional<at::Tensor> model, double lr, double momentum, double dampening,
+              double wd, double gscale, bool nesterov, bool first) {
+  check_flat(g, "grad");
+  check_master(g, w, "master");
+  if (mom.has_value()) check_master(g, *mom, "momentum");
+  int md;
+  void* mp = model_ptr(model, g, &md);
+  c10::DeviceGuard guard(g.device());
+  mv_launch_sgd(g.data_ptr(), dtype_code(g), w.data_ptr<float>(),
+                mom.has_value() ? mom->data_ptr<float>() : nullptr, mp, md, g.numel(), (float)lr,
+                (float)momentum, (float)dampening, (float)wd, (float)gscale, nesterov, first,
+                cur_stream());
+}
+
+void adam_step(at::Tensor g, at::Tensor w, at::Tensor m, at::Tensor v,
+               c10::optional<at::Tensor> model, double lr, double b1, double b2, double eps,
+               double wd, double gscale, int64_t step, bool adamw, bool keras_eps) {
+  check_flat(g, "grad");
+  check_master(g, w, "master");
+  check_master(g, m, "exp_avg");
+  check_master(g, v, "exp_avg_sq");
+  TORCH_CHECK(step >= 1, "adam_step: step must be >= 1");
+  int md;
+  void* mp = model_ptr(model, g, &md);
+  const double bc1 = 1.0 - std::pow(b1, (double)step);
+  const double bc2 = 1.0 - std::pow(b2, (double)step);
+  c10::DeviceGuard guard(g.device());
+  mv_launch_adam(g.data_ptr(), dtype_code(g), w.data_ptr<float>(), m.data_ptr<float>(),
+                 v.data_ptr<float>(), mp, md, g.numel(), (float)lr, (float)b1, (float)b2,
+                 (float)eps, (float)wd, (float)gscale, (float)bc1, (float)bc2, adamw, keras_eps,
+                 cur_stream());
+}
+
+void adadelta_step(at::Tensor g, at::Tensor w, at::Tensor sq, at::Tensor acc,
+                   c10::optional<at::Tensor> model, double lr, double rho, double eps, double wd,
+                   double gscale) {
+  check_flat(g, "grad");
+  check_master(g, w, "master");
+  check_master(g, sq, "square_avg");
+  check_master(g, acc, "acc_delta");
+  int md;
+  void* mp = model_ptr(model, g, &md);
+  c10::DeviceGuard guard(g.device());
+  mv_launch_adadelta(g.data_ptr(), dtype_code(g), w.data_ptr<float>(), sq.data_ptr<float>(),
+                     acc.data_ptr<float>(), mp, md, g.numel(), (float)lr, (float)rho, (float)eps,
+                     (float)wd, (float)gscale, cur_stream());
+}
+
+ChunkTable make_table(const at::Tensor& begin, const at::Tensor& len, const at::Tensor& seg,
+                      const at::Tensor& seg_c0, const at::Tensor& seg_nc, int64_t total) {
+  TORCH_CHECK(begin.is_cuda() && begin.scalar_type() == at::kLong && begin.is_contiguous(),
+              "chunk begin must be contiguous int64 on GPU");
+  for (const at::Tensor* t : {&len, &seg, &seg_c0, &seg_nc})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->is_contiguous(),
+                "chunk tables must be contiguous int32 on GPU");
+  TORCH_CHECK(len.numel() == begin.numel() && seg.numel() == begin.numel(),
+              "chunk table length mismatch");
+  TORCH_CHECK(seg_c0.numel() == seg_nc.numel(), "segment table length mismatch");
+  (void)total;
+  ChunkTable ct;
+  ct.begin = begin.data_ptr<int64_t>();
+  ct.len = len.data_ptr<int32_t>();
+  ct.seg = seg.data_ptr<int32_t>();
+  ct.seg_c0 = seg_c0.data_ptr<int32_t>();
+  ct.seg_nc = seg_nc.data_ptr<int32_t>();
+  ct.nchunks = (int32_t)begin.numel();
+  ct.nseg = (int32_t)seg_c0.numel();
+  return ct;
+}
+
+void lars_step(at::Tensor g, at::Tensor w, at::Tensor mom, c10::optional<at::Tensor> model,
+               at::Tensor cbeg, at::Tensor clen, at::Tensor cseg, at::Tensor seg_c0,
+               at::Tensor seg_nc, at::Tensor sflag, at::Tensor partial, at::Tensor norms, double lr,
+               double momentum, double wd, double eta, double gscale, double eps, bool first) {
+  check_flat(g, "grad");
+  check_master(g, w, "master");
+  check_master(g, mom, "momentum");
+  int md;
+  void* mp = model_ptr(model, g, &md);
+  ChunkTable ct = make_table(cbeg, clen, cseg, seg_c0, seg_nc, g.numel());
+  TORCH_CHECK(partial.scalar_type() == at::kFloat && partial.numel() >= 2 * ct.nchunks,
+              "lars: partial buffer too small");
+  TORCH_CHECK(norms.scalar_type() == at::kFloat && norms.numel() >= 2 * ct.nseg,
+              "lars: norms buffer too small");
+  TORCH_CHECK(sflag.scalar_type() == at::kInt && sflag.numel() >= ct.nseg, "lars: flags");
+  c10::DeviceGuard guard(g.device());
+  mv_launch_lars(g.data_ptr(), dtype_code(g), w.data_ptr<float>(), mom.data_ptr<float>(), mp, md,
+                 ct, sflag.data_ptr<int32_t>(), partial.data_ptr<float>(), norms.data_ptr<float>(),
+                 (float)lr, (float)momentum, (float)wd, (float)eta, (float)gscale, (float)eps, first,
+                 cur_stream());
+}
+
+void seg_dot3(at::Tensor a, at::Tensor b, at::Tensor cbeg, at::Tensor clen, at::Tensor cseg,
+              at::Tensor seg_c0, at::Tensor seg_nc, at::Tensor partial, at::Tensor out) {
+  check_flat(a, "a");
+  check_flat(b, "b");
+  TORCH_CHECK(a.numel() == b.numel() && a.scalar_type() == b.scalar_type(), "seg_dot3: a/b mismatch");
+  ChunkTable ct = make_table(cbeg, clen, cseg, seg_c0, seg_nc, a.numel());
+  TORCH_CHECK(partial.scalar_type() == at::kFloat && partial.numel() >= 3 * ct.nchunks,
+              "seg_dot3: partial buffer too small");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 3 * ct.nseg, "seg_dot3: out too small");
+  c10::DeviceGuard guard(a.device());
+  mv_launch_seg_dot3(a.data_ptr(), b.data_ptr(), dtype_code(a), ct, partial.data_ptr<float>(),
+                     out.data_ptr<float>(), cur_stream());
+}
+
+void adasum_combine(at::Tensor a, at::Tensor b, at::Tensor cbeg, at::Tensor clen, at::Tensor cseg,
+                    at::Tensor seg_c0, at::Tensor seg_nc, at::Tensor dots) {
+  check_flat(a, "a");
+  check_flat(b, "b");
+  TORCH_CHECK(a.numel() == b.numel() && a.scalar_type() == b.scalar_type(),
+              "adasum_combine: a/b mismatch");
+  ChunkTable ct = make_table(cbeg, clen, cseg, seg_c0, seg_nc, a.numel());
+  TORCH_CHECK(dots.scalar_type() == at::kFloat && dots.numel() >= 3 * ct.nseg, "adasum: dots");
+  c10::DeviceGuard guard(a.device());
+  mv_launch_adasum_combine(a.data_ptr(), b.data_ptr(), dtype_code(a), ct, dots.data_ptr<float>(),
+                           cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_mvk, m) {
+  m.doc() = "mivod hand-written gfx950 (CDNA4) kernels";
+  m.attr("CHUNK") = kChunk;
+  m.attr("MAX_TENSORS_PER_LAUNCH") = kMvMaxTensors;
+  m.def("mt_copy", &mt_copy, "multi-tensor pack/unpack with fused cast+scale");
+  m.def("flat_cast", &flat_cast, "flat cast + scale (compress/decompress)");
+  m.def("sgd_step", &sgd_step, "fused flat SGD(+momentum, nesterov) step");
+  m.def("adam_step", &adam_step, "fused flat Adam/AdamW step");
+  m.def("adadelta_step", &adadelta_step, "fused flat Adadelta step");
+  m.def("lars_step", &lars_step, "fused segmented LARS step");
+  m.def("seg_dot3", &seg_dot3, "per-segment (a.b, |a|^2, |b|^2)");
+  m.def("adasum_combine", &adasum_combine, "per-segment Adasum merge a <- ca*a + cb*b");
+}

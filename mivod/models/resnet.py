@@ -1,0 +1,107 @@
+"""ResNet-50 (v1.5 topology, 25,557,032 parameters), written from scratch.
+
+North-star workload (BASELINE.json configs 3/4): ResNet-50
+bf16 on synthetic ImageNet.  MI355X choices: NHWC (``channels_last``) so
+MIOpen / the conv kernels see the layout the matrix cores want, bf16 weights
+and activations with BatchNorm affine params and running statistics kept in
+fp32 (the mixed BN path; mivod's fused optimizer holds the fp32 master copy of
+the bf16 weights).  No torchvision (not installed), no torch.compile / Triton.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+
+def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
+    return nn.Conv2d(cin, cout, 3, stride=stride, padding=dilation, groups=groups, bias=False,
+                     dilation=dilation)
+
+
+def conv1x1(cin, cout, stride=1):
+    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, zero_init_residual=False):
+        super().__init__()
+        self.conv1 = conv1x1(inplanes, planes)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = conv3x3(planes, planes, stride)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = conv1x1(planes, planes * self.expansion)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        if zero_init_residual:
+            nn.init.zeros_(self.bn3.weight)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        out += identity
+        return self.relu(out)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, zero_init_residual=False):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, layers[0], 1, zero_init_residual)
+        self.layer2 = self._make_layer(128, layers[1], 2, zero_init_residual)
+        self.layer3 = self._make_layer(256, layers[2], 2, zero_init_residual)
+        self.layer4 = self._make_layer(512, layers[3], 2, zero_init_residual)
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Linear(512 * Bottleneck.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def _make_layer(self, planes, blocks, stride, zir):
+        down = None
+        if stride != 1 or self.inplanes != planes * Bottleneck.expansion:
+            down = nn.Sequential(conv1x1(self.inplanes, planes * Bottleneck.expansion, stride),
+                                 nn.BatchNorm2d(planes * Bottleneck.expansion))
+        layers = [Bottleneck(self.inplanes, planes, stride, down, zir)]
+        self.inplanes = planes * Bottleneck.expansion
+        for _ in range(1, blocks):
+            layers.append(Bottleneck(self.inplanes, planes, zero_init_residual=zir))
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(self.avgpool(x), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes=1000, **kw) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes, **kw)
+
+
+def resnet101(num_classes=1000, **kw) -> ResNet:
+    return ResNet((3, 4, 23, 3), num_classes, **kw)
+
+
+def to_mixed_bf16(model: nn.Module, channels_last: bool = True) -> nn.Module:
+    """bf16 conv/linear weights, fp32 BatchNorm (affine + running stats),
+    channels_last memory format."""
+    for m in model.modules():
+        if isinstance(m, (nn.Conv2d, nn.Linear)):
+            m.to(torch.bfloat16)
+    if channels_last:
+        model.to(memory_format=torch.channels_last)
+    return model

@@ -1,0 +1,408 @@
+"""``mivod.torch.DistributedOptimizer`` — the PyTorch-ROCm hook path.
+
+Parity: horovod 0.18.1 ``horovod/torch/__init__.py`` ``_DistributedOptimizer``
+(SURVEY.md §2.2 U22): wraps any ``torch.optim.Optimizer``; gradients are
+averaged across ranks as backward produces them; ``step()`` waits for the
+reductions then applies the update; ``synchronize()``, ``skip_synchronize()``,
+``backward_passes_per_step``, ``compression``, ``op`` (Average / Sum / Adasum),
+duplicate-name checks, and the "zero_grad before synchronize" assertion.
+The reference reaches the same behaviour through Keras
+(/root/reference/mnist_keras.py:86-87, tensorflow2_keras_mnist.py:57-58).
+
+MI355X design (not a translation of horovod's per-tensor async ops):
+
+* **Static schedule.**  Buckets are planned once from the parameter layout —
+  backward order, per dtype, ``MIVOD_FIRST_BUCKET_MB`` for the first bucket
+  (the last layers, to start xGMI traffic early), ``MIVOD_BUCKET_MB`` after —
+  and issued in the same order on every rank, so no per-step negotiation.
+* **One pack launch per bucket.**  ``register_post_accumulate_grad_hook``
+  marks a parameter ready; when its bucket is complete the hand-written
+  multi-tensor pack kernel (K1, fused cast = compression, fused prescale) copies
+  all its grads into the flat bucket on the compute stream.
+* **Comm stream.**  The high-priority HIP comm stream waits on the pack event,
+  runs the RCCL allreduce (xGMI ring), and — when the wrapped optimizer is a
+  ``mivod.optim.Fused*`` — immediately runs the fused optimizer kernel (K6)
+  on the reduced bucket with the 1/N average folded into its grad scale.  The
+  whole update overlaps the remaining backward; ``step()`` is then only a
+  stream wait.  Plain torch optimizers get zero-copy gradient views into the
+  reduced bucket instead.
+"""
+from __future__ import annotations
+
+import contextlib
+import threading
+import warnings
+from typing import Dict, List, Optional
+
+import torch
+
+from ..common import basics
+from ..ops import kernels as K
+from ..ops.compression import Compression
+from ..optim.fused import Arena, FusedOptimizer, _align
+from ..parallel import collectives as C
+from ..utils import timeline as TL
+
+
+class _GradArena:
+    """Gradient-only arena for plain (non-fused) optimizers."""
+
+    def __init__(self, params: List[torch.nn.Parameter], wire_dtype: torch.dtype):
+        self.params = params
+        self.offsets, o = [], 0
+        for p in params:
+            self.offsets.append(o)
+            o += _align(p.numel())
+        self.numel = o
+        self.dtype = params[0].dtype
+        self.grad_dtype = wire_dtype
+        self.device = params[0].device
+        self.grad = torch.zeros(o, dtype=wire_dtype, device=self.device)
+        self.tables: Dict[tuple, K.ChunkTable] = {}
+
+    def range_of(self, i0, i1):
+        lo = self.offsets[i0]
+        hi = self.offsets[i1] if i1 < len(self.params) else self.numel
+        return lo, hi
+
+    def slot(self, flat, i):
+        p = self.params[i]
+        return torch.as_strided(flat, p.size(), p.stride(), self.offsets[i])
+
+    def table(self, i0, i1):
+        key = (i0, i1)
+        t = self.tables.get(key)
+        if t is None:
+            lo = self.offsets[i0]
+            t = K.make_chunk_table([self.params[i].numel() for i in range(i0, i1)], self.device,
+                                   [self.offsets[i] - lo for i in range(i0, i1)])
+            self.tables[key] = t
+        return t
+
+
+class _Bucket:
+    __slots__ = ("index", "arena", "i0", "i1", "lo", "hi", "params", "pending", "launched",
+                 "order_key", "name")
+
+    def __init__(self, index, arena, i0, i1, order_key):
+        self.index = index
+        self.arena = arena
+        self.i0, self.i1 = i0, i1
+        self.lo, self.hi = arena.range_of(i0, i1)
+        self.params = arena.params[i0:i1]
+        self.pending = len(self.params)
+        self.launched = False
+        self.order_key = order_key
+        self.name = f"bucket.{index}"
+
+    @property
+    def nbytes(self):
+        return (self.hi - self.lo) * self.arena.grad.element_size()
+
+
+def plan_buckets(arenas, first_bucket_bytes: int, bucket_bytes: int, position) -> List[_Bucket]:
+    """Split every arena (params in backward order) into contiguous buckets.
+
+    The first bucket of the whole model (earliest in backward) is capped at
+    ``first_bucket_bytes``; the rest at ``bucket_bytes``.  Buckets are ordered
+    by the backward position of their first parameter, identically on all ranks.
+    """
+    raw = []
+    for a in arenas:
+        es = a.grad.element_size()
+        i0 = 0
+        cur = 0
+        for i, p in enumerate(a.params):
+            sz = _align(p.numel()) * es
+            cap = bucket_bytes
+            if cur > 0 and cur + sz > cap:
+                raw.append((a, i0, i))
+                i0, cur = i, 0
+            cur += sz
+        raw.append((a, i0, len(a.params)))
+    # split the globally-first bucket down to first_bucket_bytes
+    raw.sort(key=lambda r: min(position[id(p)] for p in r[0].params[r[1]:r[2]]))
+    if raw and first_bucket_bytes > 0:
+        a, i0, i1 = raw[0]
+        es = a.grad.element_size()
+        cur, cut = 0, i1
+        for i in range(i0, i1):
+            cur += _align(a.params[i].numel()) * es
+            if cur >= first_bucket_bytes:
+                cut = i + 1
+                break
+        if cut < i1:
+            raw[0:1] = [(a, i0, cut), (a, cut, i1)]
+    raw.sort(key=lambda r: min(position[id(p)] for p in r[0].params[r[1]:r[2]]))
+    return [_Bucket(k, a, i0, i1, min(position[id(p)] for p in a.params[i0:i1]))
+            for k, (a, i0, i1) in enumerate(raw)]
+
+
+class _DistributedOptimizerMixin:
+    """Methods mixed in front of the wrapped optimizer's class."""
+
+    # ------------------------------------------------------------------ setup
+    def _mvd_setup(self, named_parameters, compression, backward_passes_per_step, op,
+                   bucket_mb, first_bucket_mb, gradient_predivide_factor):
+        st = basics.state()
+        if not st.initialized:
+            raise ValueError(basics._NOT_INIT)
+        cfg = st.config
+        self._mvd_size = st.size
+        self._mvd_compression = compression
+        self._mvd_bpps = int(backward_passes_per_step)
+        self._mvd_op = op
+        self._mvd_predivide = float(gradient_predivide_factor)
+        if op == C.Adasum and self._mvd_predivide != 1.0:
+            raise ValueError("gradient_predivide_factor not supported with op == Adasum")
+        self._mvd_lock = threading.RLock()
+
+        all_params = [p for g in self.param_groups for p in g["params"]]
+        if named_parameters is not None:
+            named_parameters = list(named_parameters)
+            if any(not isinstance(t, tuple) or len(t) != 2 for t in named_parameters):
+                raise ValueError("named_parameters should be a sequence of tuples (name, parameter), "
+                                 "usually produced by model.named_parameters().")
+            names = [n for n, _ in named_parameters]
+            dups = sorted({n for n in names if names.count(n) > 1})
+            if dups:
+                raise ValueError("Parameter names in named_parameters must be unique. Found "
+                                 f"duplicates: {', '.join(dups)}")
+            known = {id(p) for _, p in named_parameters}
+            unnamed = [p for p in all_params if id(p) not in known]
+            if unnamed:
+                raise ValueError("named_parameters was specified, but one or more model "
+                                 "parameters were not named. Python object ids: "
+                                 f"{', '.join(str(id(p)) for p in unnamed)}")
+            self._mvd_names = {id(p): n for n, p in named_parameters}
+        else:
+            self._mvd_names = {id(p): f"allreduce.noname.{i}" for i, p in enumerate(all_params)}
+
+        trainable = [p for p in all_params if p.requires_grad]
+        # backward position: reverse registration order
+        self._mvd_position = {id(p): i for i, p in enumerate(reversed(trainable))}
+        self._mvd_fused = isinstance(self, FusedOptimizer)
+        wire = compression.wire_dtype
+        if self._mvd_fused:
+            self._mv_external_grads = True
+            arenas = self._mv_build(grad_dtype_for=wire)
+        else:
+            arenas = []
+            seen = set()
+            by_key: Dict[tuple, List[torch.nn.Parameter]] = {}
+            for p in reversed(trainable):
+                if id(p) in seen:
+                    continue
+                seen.add(id(p))
+                by_key.setdefault((p.dtype, p.device), []).append(p)
+            for (dt, _dev), ps in by_key.items():
+                arenas.append(_GradArena(ps, wire(dt)))
+        self._mvd_arenas = arenas
+        bmb = cfg.bucket_mb if bucket_mb is None else bucket_mb
+        fmb = cfg.first_bucket_mb if first_bucket_mb is None else first_bucket_mb
+        self._mvd_buckets = plan_buckets(arenas, int(fmb * 2 ** 20), int(bmb * 2 ** 20),
+                                         self._mvd_position)
+        self._mvd_where: Dict[int, tuple] = {}
+        for b in self._mvd_buckets:
+            for k, p in enumerate(b.params):
+                self._mvd_where[id(p)] = (b, b.i0 + k)
+        self._mvd_counts: Dict[int, int] = {}
+        self._mvd_next = 0
+        self._mvd_in_step = False
+        self._mvd_synchronized = False
+        self._mvd_should_sync = True
+        self._mvd_stream = st.comm_stream
+        self._mvd_done_event = None
+        self._mvd_nonfinite = None
+        self._mvd_hooks = []
+        for p in trainable:
+            self._mvd_hooks.append(p.register_post_accumulate_grad_hook(self._mvd_hook))
+        TL.note_plan(self._mvd_buckets)
+
+    # --------------------------------------------------------------- hot path
+    def _mvd_hook(self, p: torch.Tensor):
+        with self._mvd_lock:
+            c = self._mvd_counts.get(id(p), 0) + 1
+            self._mvd_counts[id(p)] = c
+            if c < self._mvd_bpps:
+                return
+            if c > self._mvd_bpps:
+                raise AssertionError(
+                    "Gradients were computed more than backward_passes_per_step times before call "
+                    "to step(). Increase backward_passes_per_step to accumulate gradients locally.")
+            b, _ = self._mvd_where[id(p)]
+            b.pending -= 1
+            if b.pending == 0:
+                self._mvd_launch_ready()
+
+    def _mvd_launch_ready(self):
+        bs = self._mvd_buckets
+        while self._mvd_next < len(bs) and bs[self._mvd_next].pending == 0:
+            self._mvd_launch(bs[self._mvd_next])
+            self._mvd_next += 1
+
+    def _mvd_launch(self, b: _Bucket):
+        if not self._mvd_in_step:
+            self._mvd_in_step = True
+            if self._mvd_fused:
+                self._mv_begin_step()
+        a = b.arena
+        size = self._mvd_size
+        prescale = 1.0 / self._mvd_predivide if self._mvd_op == C.Average else 1.0
+        groups: Dict[torch.dtype, tuple] = {}
+        with torch.no_grad():
+            for k, p in enumerate(b.params):
+                i = b.i0 + k
+                g = p.grad
+                lo = a.offsets[i]
+                if g is None:
+                    a.grad[lo:lo + p.numel()].zero_()
+                    continue
+                if g.data_ptr() == a.grad.data_ptr() + lo * a.grad.element_size() and \
+                        g.dtype == a.grad.dtype and g.stride() == p.stride():
+                    if prescale != 1.0:
+                        g.mul_(prescale)
+                    continue  # gradient already lives in its bucket slot (accumulated in place)
+                if g.stride() != p.stride() or not K.is_dense(g):
+                    g = torch.empty_like(p, dtype=g.dtype).copy_(g)
+                ent = groups.setdefault(g.dtype, ([], []))
+                ent[0].append(g)
+                ent[1].append(lo)
+            for dt, (gl, ol) in groups.items():
+                K.pack(gl, a.grad, ol, scale=prescale)
+            if self._mvd_fused:
+                for p in b.params:
+                    p.grad = None            # freed on the compute stream after the pack
+        flat = a.grad[b.lo:b.hi]
+        cuda = flat.is_cuda and self._mvd_stream is not None
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            ctx = torch.cuda.stream(self._mvd_stream)
+        else:
+            ctx = contextlib.nullcontext()
+        with ctx:
+            if cuda:
+                self._mvd_stream.wait_event(ev)
+            if size > 1:
+                if self._mvd_op == C.Adasum:
+                    C.allreduce_(flat, C.Adasum, adasum_table=a.table(b.i0, b.i1))
+                elif self._mvd_fused:
+                    C.allreduce_(flat, C.Sum)
+                else:
+                    C.allreduce_(flat, C.Average if self._mvd_op == C.Average else C.Sum)
+            if self._mvd_fused:
+                gscale = 1.0
+                if self._mvd_op == C.Average:
+                    gscale = self._mvd_predivide / size
+                self._mv_apply(a, b.i0, b.i1, gscale)
+            else:
+                post = self._mvd_predivide if (self._mvd_op == C.Average and size > 1) else 1.0
+                if post != 1.0:
+                    flat.mul_(post)
+                self._mvd_expose_grads(b)
+            if cuda:
+                ev2 = torch.cuda.Event()
+                ev2.record()
+                self._mvd_done_event = ev2
+        b.launched = True
+
+    def _mvd_expose_grads(self, b: _Bucket):
+        """Plain optimizers: p.grad := reduced values (zero-copy view when the
+        wire dtype equals the grad dtype, fused unpack + decompress otherwise)."""
+        a = b.arena
+        same = a.grad.dtype == a.dtype
+        if same:
+            for k, p in enumerate(b.params):
+                p.grad = a.slot(a.grad, b.i0 + k)
+            return
+        outs, offs = [], []
+        for k, p in enumerate(b.params):
+            i = b.i0 + k
+            if p.grad is None or p.grad.dtype != p.dtype or p.grad.stride() != p.stride():
+                p.grad = torch.empty_like(p)
+            outs.append(p.grad)
+            offs.append(a.offsets[i])
+        K.unpack(outs, a.grad, offs)
+
+    # -------------------------------------------------------------- user API
+    def synchronize(self):
+        with self._mvd_lock:
+            if any(c != self._mvd_bpps for c in self._mvd_counts.values()) and \
+                    self._mvd_counts and self._mvd_bpps > 1:
+                pass  # partial accumulation windows are allowed; missing grads reduce as zeros
+            for b in self._mvd_buckets:
+                if not b.launched:
+                    b.pending = 0
+            self._mvd_launch_ready()
+            if self._mvd_stream is not None and torch.cuda.is_available():
+                torch.cuda.current_stream().wait_stream(self._mvd_stream)
+            if self._mvd_fused:
+                self._mv_end_step()
+            for b in self._mvd_buckets:
+                b.launched = False
+                b.pending = len(b.params)
+            self._mvd_counts.clear()
+            self._mvd_next = 0
+            self._mvd_in_step = False
+            self._mvd_synchronized = True
+
+    @contextlib.contextmanager
+    def skip_synchronize(self):
+        """Use after an explicit ``synchronize()`` (e.g. to clip gradients)."""
+        self._mvd_should_sync = False
+        try:
+            yield
+        finally:
+            self._mvd_should_sync = True
+
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if self._mvd_should_sync:
+            if self._mvd_synchronized:
+                warnings.warn("optimizer.step() called without a loss.backward() since the last "
+                              "synchronize(); re-using the last reduced gradients.")
+            else:
+                self.synchronize()
+        elif not self._mvd_synchronized:
+            raise AssertionError("skip_synchronize() used without a preceding synchronize()")
+        self._mvd_synchronized = False
+        if self._mvd_fused:
+            return loss           # the fused update already ran on the comm stream
+        super().step()
+        return loss
+
+    def zero_grad(self, set_to_none: bool = True):
+        if self._mvd_in_step:
+            raise AssertionError("optimizer.zero_grad() was called after loss.backward() but before "
+                                 "optimizer.step() or optimizer.synchronize(). This is prohibited "
+                                 "as it can cause a race condition.")
+        return super().zero_grad(set_to_none=set_to_none)
+
+    def bucket_plan(self):
+        """[(name, nbytes, [param names])] of the static schedule."""
+        return [(b.name, b.nbytes, [self._mvd_names[id(p)] for p in b.params])
+                for b in self._mvd_buckets]
+
+
+def DistributedOptimizer(optimizer, named_parameters=None, compression=Compression.none,
+                         backward_passes_per_step: int = 1, op=C.Average, bucket_mb=None,
+                         first_bucket_mb=None, gradient_predivide_factor: float = 1.0):
+    """Wrap ``optimizer`` so gradients are averaged (``op``) across all ranks.
+
+    Returns an instance of a dynamically created subclass of the optimizer's
+    class (same class name, so ``isinstance`` and pickled configs keep working),
+    carrying over the optimizer's state and param groups.
+    """
+    base = optimizer.__class__
+    if isinstance(optimizer, _DistributedOptimizerMixin):
+        raise ValueError("optimizer is already a mivod DistributedOptimizer")
+    cls = type(base.__name__, (_DistributedOptimizerMixin, base), {"__module__": base.__module__})
+    obj = cls.__new__(cls)
+    obj.__dict__.update(optimizer.__dict__)
+    obj._mvd_setup(named_parameters, compression, backward_passes_per_step, op, bucket_mb,
+                   first_bucket_mb, gradient_predivide_factor)
+    return obj
