@@ -96,8 +96,12 @@ def main():
         return loss
 
     t_w0 = time.perf_counter()
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         loss = step()
+        if rank == 0 and (i < 3 or i == args.warmup - 1):
+            torch.cuda.synchronize()
+            print(f"[bench] warmup step {i} done at {time.perf_counter() - t_w0:.1f}s",
+                  file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     warm_s = time.perf_counter() - t_w0
 
@@ -122,7 +126,7 @@ def main():
     ms = elapsed / max(args.steps, 1) * 1000.0
     ips = args.batch * size * args.steps / elapsed
     if rank == 0:
-        print(f"[bench] warmup {args.warmup} steps {warm_s:.1f}s; loss {float(loss):.4f}; "
+        print(f"[bench] warmup {args.warmup} steps {warm_s:.1f}s; loss {float(loss.detach()):.4f}; "
               f"{ms:.2f} ms/step; buckets={len(opt.bucket_plan())}", file=sys.stderr)
         rec = {
             "metric": BASELINE_METRIC,

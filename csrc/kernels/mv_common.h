@@ -20,8 +20,6 @@ constexpr int kChunk = 4096;       // elements per workgroup (2 steps of 256x8)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T> struct DT;
 template <> struct DT<float> { static constexpr Dtype v = F32; };
@@ -65,16 +63,21 @@ __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
   *reinterpret_cast<f32x4*>(p) = a;
   *reinterpret_cast<f32x4*>(p + 4) = b;
 }
+// Packed RNE f32x2 -> bf16x2 on gfx950 (lo <- a, hi <- b).  Written as inline
+// asm: ROCm 7.2 clang mis-lowers __builtin_convertvector(f32x2 -> bf16x2) inside
+// unrolled loops (it converted only the even elements: caught by
+// tests/test_kernels_gpu.py::test_pack_unpack_cast_scale).
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ void store8(__bf16* p, const float (&v)[8]) {
-  u16x8 o;
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    f32x2 f = {v[j], v[j + 1]};
-    bf16x2 h = __builtin_convertvector(f, bf16x2);   // v_cvt_pk_bf16_f32
-    o[j] = __builtin_bit_cast(unsigned short, h[0]);
-    o[j + 1] = __builtin_bit_cast(unsigned short, h[1]);
-  }
-  *reinterpret_cast<u16x8*>(p) = o;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 o = {cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]), cvt_pk_bf16(v[4], v[5]),
+             cvt_pk_bf16(v[6], v[7])};
+  *reinterpret_cast<u32x4*>(p) = o;
 }
 __device__ __forceinline__ void store8(_Float16* p, const float (&v)[8]) {
   u16x8 o;

@@ -2,7 +2,7 @@
 
 Parity: horovod 0.18.1 ``horovod/torch``.
 """
-from ..common.basics import (cross_rank, cross_size, gloo_enabled, init, is_initialized,
+from ..common.basics import (comm_stream, cross_rank, cross_size, device, gloo_enabled, init, is_initialized,
                              local_rank, local_size, mpi_enabled, mpi_threads_supported,
                              nccl_built, rank, rocm_built, shutdown, size)
 from ..ops.compression import Compression

@@ -52,7 +52,7 @@ def test_resnet50_bf16_step(hvd, cuda):
     from mivod.models.resnet import resnet50, to_mixed_bf16
     from mivod.optim import FusedSGD
     model = to_mixed_bf16(resnet50(num_classes=100)).to(cuda)
-    opt = hvd.DistributedOptimizer(FusedSGD(model.parameters(), lr=0.1, momentum=0.9),
+    opt = hvd.DistributedOptimizer(FusedSGD(model.parameters(), lr=0.01, momentum=0.9),
                                    named_parameters=model.named_parameters())
     assert len(opt.bucket_plan()) >= 2
     x = torch.randn(8, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(
@@ -64,7 +64,7 @@ def test_resnet50_bf16_step(hvd, cuda):
         loss.backward()
         opt.step()
         opt.zero_grad()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     assert all(map(lambda v: v == v, losses))
     assert losses[-1] < losses[0], losses
 
