@@ -1,0 +1,106 @@
+// pybind11 module mivod._mvcore: the native engine core (no GPU dependency).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "controller.h"
+#include "timeline.h"
+
+namespace py = pybind11;
+using namespace mvcore;
+
+namespace {
+
+// request tuple: (name, kind, dtype, shape, root, op, device, nbytes)
+Request to_request(const py::handle& h) {
+  auto t = py::reinterpret_borrow<py::tuple>(h);
+  if (t.size() != 8) throw std::invalid_argument("mivod request must be an 8-tuple");
+  Request r;
+  r.name = t[0].cast<std::string>();
+  r.kind = (uint8_t)t[1].cast<int>();
+  r.dtype = t[2].cast<std::string>();
+  for (auto d : t[3]) r.shape.push_back(d.cast<int64_t>());
+  r.root = t[4].cast<int32_t>();
+  r.op = t[5].cast<int32_t>();
+  r.device = t[6].cast<int32_t>();
+  r.nbytes = t[7].cast<int64_t>();
+  return r;
+}
+
+py::list to_py(const std::vector<Response>& rs) {
+  py::list out;
+  for (const auto& r : rs) {
+    py::list names;
+    for (const auto& n : r.names) names.append(n);
+    out.append(py::make_tuple((int)r.kind, names, r.error));
+  }
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_mvcore, m) {
+  m.doc() = "mivod native engine core: TCP coordinator, stall inspector, timeline";
+
+  py::class_<Timeline, std::shared_ptr<Timeline>>(m, "Timeline")
+      .def(py::init<const std::string&, bool>(), py::arg("path"), py::arg("mark_cycles") = false)
+      .def("start", &Timeline::start, py::arg("name"), py::arg("phase"), py::arg("args") = "",
+           py::call_guard<py::gil_scoped_release>())
+      .def("activity", &Timeline::activity, py::call_guard<py::gil_scoped_release>())
+      .def("end", &Timeline::end, py::call_guard<py::gil_scoped_release>())
+      .def("instant", &Timeline::instant, py::call_guard<py::gil_scoped_release>())
+      .def("mark_cycle", &Timeline::mark_cycle, py::call_guard<py::gil_scoped_release>())
+      .def("close", &Timeline::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("events_written", &Timeline::events_written);
+
+  py::class_<ControllerConfig>(m, "ControllerConfig")
+      .def(py::init<>())
+      .def_readwrite("rank", &ControllerConfig::rank)
+      .def_readwrite("size", &ControllerConfig::size)
+      .def_readwrite("host", &ControllerConfig::host)
+      .def_readwrite("port", &ControllerConfig::port)
+      .def_readwrite("fusion_threshold", &ControllerConfig::fusion_threshold)
+      .def_readwrite("stall_check_s", &ControllerConfig::stall_check_s)
+      .def_readwrite("stall_shutdown_s", &ControllerConfig::stall_shutdown_s)
+      .def_readwrite("stall_check", &ControllerConfig::stall_check)
+      .def_readwrite("connect_timeout_s", &ControllerConfig::connect_timeout_s);
+
+  py::class_<Controller>(m, "Controller")
+      .def(py::init<const ControllerConfig&>())
+      .def("listen", &Controller::listen, py::call_guard<py::gil_scoped_release>())
+      .def("connect", &Controller::connect, py::call_guard<py::gil_scoped_release>())
+      .def("set_timeline", &Controller::set_timeline)
+      .def("negotiate",
+           [](Controller& c, py::list reqs, bool shutdown) {
+             std::vector<Request> rs;
+             rs.reserve(reqs.size());
+             for (auto h : reqs) rs.push_back(to_request(h));
+             bool all = false;
+             std::vector<Response> out;
+             {
+               py::gil_scoped_release nogil;
+               out = c.negotiate(rs, shutdown, &all);
+             }
+             return py::make_tuple(to_py(out), all);
+           },
+           py::arg("requests"), py::arg("shutdown") = false)
+      .def("coordinate_for_test",
+           [](Controller& c, py::list per_rank) {
+             std::vector<std::vector<Request>> pr;
+             for (auto lst : per_rank) {
+               std::vector<Request> rs;
+               for (auto h : lst) rs.push_back(to_request(h));
+               pr.push_back(rs);
+             }
+             return to_py(c.coordinate_for_test(pr));
+           })
+      .def("last_stalls",
+           [](const Controller& c) {
+             py::list out;
+             for (const auto& s : c.last_stalls())
+               out.append(py::make_tuple(s.name, s.missing_ranks, s.age_s));
+             return out;
+           })
+      .def_property_readonly("cycles", &Controller::cycles)
+      .def_property_readonly("cache_hits", &Controller::cache_hits)
+      .def("close", &Controller::close, py::call_guard<py::gil_scoped_release>());
+}

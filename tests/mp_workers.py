@@ -1,0 +1,306 @@
+"""Multi-rank scenarios, run as `python tests/mp_workers.py <scenario>` by
+tests/test_multiprocess.py in N processes (gloo on CPU).  Each scenario asserts
+and prints "OK <rank>" at the end.  Reference behaviour: horovod's
+test_torch.py style (rank-seeded tensors, sum == size * x, average == x, error
+cases raise on every rank rather than hang)."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import mivod.torch as hvd  # noqa: E402
+
+
+def _close(a, b, tol=1e-5):
+    torch.testing.assert_close(a, b, rtol=tol, atol=tol)
+
+
+def basics():
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    assert n == int(os.environ["WORLD_SIZE"]) and r == int(os.environ["RANK"])
+    assert hvd.local_rank() == r and hvd.local_size() == n
+    assert hvd.cross_size() == 1 and hvd.cross_rank() == 0
+    for dt in (torch.float32, torch.float64, torch.int32, torch.int64, torch.float16,
+               torch.bfloat16):
+        for dims in (1, 2, 3):
+            torch.manual_seed(1234)
+            x = (torch.rand([17] * dims) * 100).to(dt)
+            s = hvd.allreduce(x, op=hvd.Sum, name=f"sum.{dt}.{dims}")
+            tol = 1e-2 if dt in (torch.float16, torch.bfloat16) else 1e-5
+            _close(s.double(), (x.double() * n), tol=tol * 100 if dt == torch.bfloat16 else tol)
+            if dt.is_floating_point:
+                a = hvd.allreduce(x, name=f"avg.{dt}.{dims}")
+                _close(a.double(), x.double(), tol=tol * 10)
+    # rank-dependent average
+    x = torch.full((5,), float(r))
+    _close(hvd.allreduce(x), torch.full((5,), (n - 1) / 2.0))
+    # in-place + async + many names (fusion)
+    hs = [hvd.allreduce_async_(torch.full((100 + i,), float(r + i)), name=f"fused.{i}",
+                               op=hvd.Sum) for i in range(20)]
+    for i, h in enumerate(hs):
+        out = hvd.synchronize(h)
+        _close(out, torch.full((100 + i,), float(sum(rr + i for rr in range(n)))))
+    # compression
+    y = torch.randn(1000)
+    z = hvd.allreduce(y, compression=hvd.Compression.fp16, name="fp16c")
+    _close(z, y.half().float(), tol=1e-3)
+    # pre/post scale
+    p = hvd.allreduce(torch.ones(4), op=hvd.Sum, prescale_factor=2.0, postscale_factor=0.5)
+    _close(p, torch.full((4,), float(n)))
+    # allgather, ragged first dim
+    g = hvd.allgather(torch.full((r + 1, 3), float(r)), name="ag")
+    assert g.shape == (sum(range(1, n + 1)), 3)
+    off = 0
+    for rr in range(n):
+        _close(g[off:off + rr + 1], torch.full((rr + 1, 3), float(rr)))
+        off += rr + 1
+    # broadcast
+    b = hvd.broadcast(torch.full((3,), float(r)), root_rank=n - 1, name="bc")
+    _close(b, torch.full((3,), float(n - 1)))
+    t = torch.full((2, 2), float(r))
+    hvd.broadcast_(t, 0)
+    _close(t, torch.zeros(2, 2))
+    # alltoall
+    a2a = hvd.alltoall(torch.arange(n * 2, dtype=torch.float32) + 100 * r)
+    exp = torch.cat([torch.arange(2 * r, 2 * r + 2, dtype=torch.float32) + 100 * rr
+                     for rr in range(n)])
+    _close(a2a, exp)
+    # autograd through allreduce
+    w = torch.ones(3, requires_grad=True)
+    hvd.allreduce(w * (r + 1), op=hvd.Sum).sum().backward()
+    # d/dw sum(allreduce_sum(w*(r+1))) = allreduce_sum(ones) * (r+1) = n*(r+1)
+    _close(w.grad, torch.full((3,), float(n * (r + 1))))
+    # objects
+    o = hvd.broadcast_object({"rank": r, "v": [1, 2]}, root_rank=0)
+    assert o == {"rank": 0, "v": [1, 2]}
+    objs = hvd.allgather_object(r * 10)
+    assert objs == [rr * 10 for rr in range(n)]
+    hvd.shutdown()
+    print("OK", r)
+
+
+def errors():
+    hvd.init()
+    r = hvd.rank()
+    # mismatched shapes -> error on every rank, no hang
+    try:
+        hvd.allreduce(torch.ones(3 + r), name="bad.shape")
+        raise AssertionError("expected failure")
+    except hvd.HorovodInternalError as e:
+        assert "Mismatched allreduce tensor shapes" in str(e), str(e)
+    try:
+        hvd.allreduce(torch.ones(3, dtype=torch.float32 if r == 0 else torch.float64),
+                      name="bad.dtype")
+        raise AssertionError("expected failure")
+    except hvd.HorovodInternalError as e:
+        assert "Mismatched data types" in str(e), str(e)
+    try:
+        hvd.broadcast(torch.ones(3), root_rank=r, name="bad.root")
+        raise AssertionError("expected failure")
+    except hvd.HorovodInternalError as e:
+        assert "root rank" in str(e), str(e)
+    # the engine still works afterwards
+    _close(hvd.allreduce(torch.ones(3), name="good"), torch.ones(3))
+    hvd.shutdown()
+    print("OK", r)
+
+
+def out_of_order():
+    """Ranks submit the same names in different orders; negotiation matches them."""
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    names = [f"t{i}" for i in range(8)]
+    order = names if r % 2 == 0 else list(reversed(names))
+    hs = {nm: hvd.allreduce_async(torch.full((10,), float(r * 10 + int(nm[1:]))), name=nm,
+                                  op=hvd.Sum) for nm in order}
+    for nm in names:
+        i = int(nm[1:])
+        _close(hvd.synchronize(hs[nm]), torch.full((10,), float(sum(rr * 10 + i
+                                                                      for rr in range(n)))))
+    hvd.shutdown()
+    print("OK", r)
+
+
+def stall():
+    os.environ["HOROVOD_STALL_CHECK_TIME_SECONDS"] = "1"
+    hvd.init()
+    r = hvd.rank()
+    from mivod.common import basics
+    eng = basics.state().engine
+    if r == 0:
+        h = hvd.allreduce_async(torch.ones(2), name="late")
+        time.sleep(2.5)
+        stalls = eng.controller.last_stalls()
+        assert any(s[0] == "late" and 1 in s[1] for s in stalls), stalls
+        _close(hvd.synchronize(h), torch.ones(2))
+    else:
+        time.sleep(3.0)
+        _close(hvd.allreduce(torch.ones(2), name="late"), torch.ones(2))
+    hvd.shutdown()
+    print("OK", r)
+
+
+def _toy(seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8), torch.nn.ReLU(),
+                               torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 10))
+
+
+def _make_opt(kind, params):
+    from mivod.optim import FusedAdam, FusedLARS, FusedSGD
+    if kind == "fused_sgd":
+        return FusedSGD(params, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    if kind == "fused_adam":
+        return FusedAdam(params, lr=1e-2)
+    if kind == "fused_lars":
+        return FusedLARS(params, lr=0.5, momentum=0.9, weight_decay=1e-4)
+    if kind == "torch_sgd":
+        return torch.optim.SGD(params, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    if kind == "torch_adam":
+        return torch.optim.Adam(params, lr=1e-2)
+    raise ValueError(kind)
+
+
+def dist_optimizer():
+    """Params after k steps equal a single-process run on the averaged gradient
+    (BN in train mode sees each rank's own batch, exactly as in DP)."""
+    import copy
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    for kind in ("fused_sgd", "torch_sgd", "fused_adam", "torch_adam", "fused_lars"):
+        comps = (hvd.Compression.none,) if "adam" in kind else (hvd.Compression.none,
+                                                                  hvd.Compression.fp16)
+        # (Adam normalises each coordinate, so fp16 rounding of tiny gradients is
+        # not comparable elementwise; fp16 wire is covered with SGD / LARS.)
+        for comp in comps:
+            base = _toy(0)
+            m = copy.deepcopy(base)
+            opt = hvd.DistributedOptimizer(_make_opt(kind, m.parameters()),
+                                           named_parameters=m.named_parameters(),
+                                           compression=comp, bucket_mb=0.005,
+                                           first_bucket_mb=0.001)
+            hvd.broadcast_parameters(m.state_dict(), 0)
+            # reference: same model, per-rank grads averaged by hand
+            ref = copy.deepcopy(base)
+            ref_opt = _make_opt(kind, ref.parameters())
+            data = []
+            for rr in range(n):
+                g = torch.Generator().manual_seed(100 + rr)
+                data.append((torch.randn(4, 3, 8, 8, generator=g), torch.randint(0, 10, (4,),
+                                                                                  generator=g)))
+            for step in range(3):
+                x, y = data[r]
+                opt.zero_grad()
+                torch.nn.functional.cross_entropy(m(x), y).backward()
+                opt.step()
+                grads = None
+                for rr in range(n):
+                    refc = copy.deepcopy(ref)
+                    refc.zero_grad()
+                    torch.nn.functional.cross_entropy(refc(data[rr][0]), data[rr][1]).backward()
+                    gs = [p.grad.clone() for p in refc.parameters()]
+                    if comp is hvd.Compression.fp16:
+                        gs = [g.half().float() for g in gs]
+                    grads = gs if grads is None else [a + b for a, b in zip(grads, gs)]
+                    if rr == r:
+                        ref.load_state_dict(refc.state_dict())  # own BN running stats
+                for p, g in zip(ref.parameters(), grads):
+                    p.grad = g / n
+                ref_opt.step()
+            tol = 2e-3 if comp is hvd.Compression.fp16 else 2e-5
+            for (nm, p), q in zip(m.named_parameters(), ref.parameters()):
+                torch.testing.assert_close(p.detach(), q.detach(), rtol=tol, atol=tol,
+                                           msg=lambda s: f"{kind} {comp.__name__} {nm}: {s}")
+            # all ranks bit-identical
+            flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+            allf = hvd.allgather(flat.unsqueeze(0))
+            assert torch.equal(allf[0], allf[-1]), kind
+    hvd.shutdown()
+    print("OK", r)
+
+
+def broadcast_state():
+    import copy
+    hvd.init()
+    r = hvd.rank()
+    for kind in ("fused_sgd", "torch_sgd", "torch_adam", "fused_adam"):
+        m = _toy(seed=r)  # different init per rank
+        opt = _make_opt(kind, m.parameters())
+        opt.param_groups[0]["lr"] = 0.1 * (r + 1)
+        # take a local step so state differs per rank
+        torch.nn.functional.cross_entropy(m(torch.randn(2, 3, 8, 8)), torch.tensor([1, 2])).backward()
+        opt.step()
+        hvd.broadcast_parameters(m.state_dict(), root_rank=0)
+        hvd.broadcast_optimizer_state(opt, root_rank=0)
+        sd = copy.deepcopy(m.state_dict())
+        allsd = hvd.allgather_object({k: v.clone() for k, v in sd.items()})
+        for k in sd:
+            assert torch.equal(allsd[0][k], allsd[-1][k]), (kind, k)
+        assert abs(opt.param_groups[0]["lr"] - 0.1) < 1e-12, opt.param_groups[0]["lr"]
+        st = opt.state_dict()["state"]
+        allst = hvd.allgather_object({k: {kk: (vv.clone() if torch.is_tensor(vv) else vv)
+                                          for kk, vv in v.items()} for k, v in st.items()})
+        for pid in allst[0]:
+            for kk, vv in allst[0][pid].items():
+                ov = allst[-1][pid][kk]
+                if torch.is_tensor(vv):
+                    assert torch.equal(vv, ov), (kind, pid, kk)
+    hvd.shutdown()
+    print("OK", r)
+
+
+def adasum():
+    import numpy as np
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    vecs = [np.random.RandomState(7 + rr).randn(1000).astype(np.float64) for rr in range(n)]
+
+    def comb(a, b):
+        d = a @ b
+        na, nb = a @ a, b @ b
+        return (1 - d / (2 * na)) * a + (1 - d / (2 * nb)) * b
+
+    cur = list(vecs)
+    while len(cur) > 1:
+        cur = [comb(cur[i], cur[i + 1]) for i in range(0, len(cur), 2)]
+    out = hvd.allreduce(torch.tensor(vecs[r], dtype=torch.float32), op=hvd.Adasum, name="ada")
+    np.testing.assert_allclose(out.numpy(), cur[0], rtol=1e-4, atol=1e-4)
+    # identical gradients: adasum(g, g) = g
+    g = torch.ones(50)
+    _close(hvd.allreduce(g, op=hvd.Adasum, name="ada2"), g)
+    # orthogonal gradients: sum
+    e = torch.zeros(n * 4)
+    e[r * 4:(r + 1) * 4] = 1.0
+    _close(hvd.allreduce(e, op=hvd.Adasum, name="ada3"), torch.ones(n * 4))
+    hvd.shutdown()
+    print("OK", r)
+
+
+def timeline():
+    path = os.environ["HOROVOD_TIMELINE"]
+    hvd.init()
+    for i in range(3):
+        hvd.allreduce(torch.ones(10) * i, name=f"tl.{i}")
+    hvd.shutdown()
+    from mivod.utils import timeline as TL
+    TL.stop_timeline()
+    if hvd_rank() == 0:
+        import json
+        ev = json.load(open(path))
+        names = {e.get("name") for e in ev}
+        assert "NEGOTIATE_allreduce" in names, names
+        assert "QUEUE" in names and ("GLOO_ALLREDUCE" in names or "NCCL_ALLREDUCE" in names), names
+    print("OK", hvd_rank())
+
+
+def hvd_rank():
+    return int(os.environ.get("RANK", "0"))
+
+
+if __name__ == "__main__":
+    globals()[sys.argv[1]]()

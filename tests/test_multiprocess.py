@@ -1,0 +1,86 @@
+"""Multi-process CPU tier (T2): N local ranks over gloo, as horovod's own tests
+run `mpirun -np 2 pytest`.  Scenarios live in tests/mp_workers.py."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_ranks(scenario, n=2, timeout=240, extra_env=None):
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(r),
+                    "WORLD_SIZE": str(n), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(n),
+                    "MIVOD_TRANSPORT": "gloo", "OMP_NUM_THREADS": "1",
+                    "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
+        env.pop("HOROVOD_RANK", None)
+        if extra_env:
+            env.update(extra_env)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_workers.py"),
+                                       scenario], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, (p, out) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0 and f"OK {r}" in out, f"rank {r} rc={p.returncode}\n{out}"
+    return outs
+
+
+def test_basics_2ranks():
+    run_ranks("basics", 2)
+
+
+def test_basics_4ranks():
+    run_ranks("basics", 4)
+
+
+def test_negotiation_errors():
+    run_ranks("errors", 2)
+
+
+def test_out_of_order_submission():
+    run_ranks("out_of_order", 3)
+
+
+def test_stall_inspector():
+    run_ranks("stall", 2)
+
+
+def test_distributed_optimizer_matches_averaged_reference():
+    run_ranks("dist_optimizer", 2, timeout=400)
+
+
+def test_broadcast_parameters_and_optimizer_state():
+    run_ranks("broadcast_state", 2)
+
+
+def test_adasum_4ranks():
+    run_ranks("adasum", 4)
+
+
+def test_timeline(tmp_path):
+    path = str(tmp_path / "timeline.json")
+    run_ranks("timeline", 2, extra_env={"HOROVOD_TIMELINE": path})
+    assert os.path.getsize(path) > 0
