@@ -8,6 +8,7 @@
 
 #include <vector>
 
+#include "mv_bn.h"
 #include "mv_kernels.h"
 
 namespace {
@@ -234,6 +235,118 @@ void adasum_combine(at::Tensor a, at::Tensor b, at::Tensor cbeg, at::Tensor clen
                            cur_stream());
 }
 
+// ---------------------------------------------------------------------------
+// Fused NHWC BatchNorm (+ residual add) (+ ReLU), bf16 activations, fp32 params
+// ---------------------------------------------------------------------------
+int64_t bn_check_act(const at::Tensor& t, const char* what, int64_t* C) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, "bn: ", what,
+              " must be a bf16 GPU tensor");
+  TORCH_CHECK(t.dim() >= 2, "bn: ", what, " must have a channel dim");
+  const bool ok = (t.dim() == 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast)) ||
+                  (t.dim() == 2 && t.is_contiguous());
+  TORCH_CHECK(ok, "bn: ", what, " must be channels_last 4-D or contiguous 2-D");
+  *C = t.size(1);
+  TORCH_CHECK(*C % 8 == 0, "bn: channel count must be a multiple of 8");
+  return t.numel() / *C;
+}
+
+const float* opt_f32(const c10::optional<at::Tensor>& t, int64_t C, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+              t->numel() == C, "bn: ", what, " must be a contiguous fp32 [C] GPU tensor");
+  return t->data_ptr<float>();
+}
+
+std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> gamma,
+                                     c10::optional<at::Tensor> beta,
+                                     c10::optional<at::Tensor> running_mean,
+                                     c10::optional<at::Tensor> running_var, double momentum,
+                                     double eps, bool relu, c10::optional<at::Tensor> residual) {
+  int64_t C;
+  const int64_t M = bn_check_act(x, "x", &C);
+  TORCH_CHECK(M > 0, "bn: empty input");
+  c10::DeviceGuard guard(x.device());
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    int64_t C2;
+    bn_check_act(*residual, "residual", &C2);
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->strides() == x.strides(),
+                "bn: residual must match x in shape and layout");
+    rp = residual->data_ptr();
+  }
+  auto fo = x.options().dtype(at::kFloat);
+  const int P = mv_bn_partials(M, (int)C);
+  at::Tensor partial = at::empty({(int64_t)P * 2 * C}, fo);
+  at::Tensor vec = at::empty({4, C}, fo);   // save_mean, save_invstd, scale, bias
+  at::Tensor y = at::empty_like(x);
+  float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
+  float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "bn: running_mean/var must both be given");
+  mv_bn_fwd_train(x.data_ptr(), rp, y.data_ptr(), M, (int)C, rm, rv, opt_f32(gamma, C, "weight"),
+                  opt_f32(beta, C, "bias"), (float)momentum, (float)eps, relu,
+                  partial.data_ptr<float>(), P, vec[0].data_ptr<float>(),
+                  vec[1].data_ptr<float>(), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
+                  cur_stream());
+  return {y, vec};
+}
+
+at::Tensor bn_apply(at::Tensor x, at::Tensor scale, at::Tensor bias, bool relu,
+                    c10::optional<at::Tensor> residual) {
+  int64_t C;
+  const int64_t M = bn_check_act(x, "x", &C);
+  c10::DeviceGuard guard(x.device());
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->strides() == x.strides() &&
+                residual->scalar_type() == at::kBFloat16, "bn: residual must match x");
+    rp = residual->data_ptr();
+  }
+  at::Tensor y = at::empty_like(x);
+  mv_bn_apply(x.data_ptr(), rp, y.data_ptr(), M, (int)C, opt_f32(scale, C, "scale"),
+              opt_f32(bias, C, "bias"), relu, cur_stream());
+  return y;
+}
+
+// returns {dx, dgamma, dbeta, dz}; dz defined only for mode 2 (residual branch grad)
+std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
+                               c10::optional<at::Tensor> y, at::Tensor vec,
+                               c10::optional<at::Tensor> gamma, bool need_affine_grad) {
+  int64_t C, C2;
+  const int64_t M = bn_check_act(x, "x", &C);
+  bn_check_act(dy, "grad", &C2);
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides(), "bn: grad layout mismatch");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "bn: bad mode");
+  TORCH_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() &&
+              vec.numel() == 4 * C, "bn: saved stats must be fp32 [4, C]");
+  const void* yp = nullptr;
+  if (mode == 2) {
+    TORCH_CHECK(y.has_value() && y->defined() && y->sizes() == x.sizes() &&
+                y->strides() == x.strides() && y->scalar_type() == at::kBFloat16,
+                "bn: mode 2 needs the saved output");
+    yp = y->data_ptr();
+  }
+  c10::DeviceGuard guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  const int P = mv_bn_partials(M, (int)C);
+  at::Tensor partial = at::empty({(int64_t)P * 2 * C}, fo);
+  at::Tensor work = at::empty({5, C}, fo);  // dgamma, dbeta, a, b, c
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dz;
+  if (mode == 2) dz = at::empty_like(x);
+  mv_bn_bwd((int)mode, dy.data_ptr(), x.data_ptr(), yp, mode == 2 ? dz.data_ptr() : nullptr,
+            dx.data_ptr(), M, (int)C, vec[0].data_ptr<float>(), vec[1].data_ptr<float>(),
+            opt_f32(gamma, C, "weight"), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
+            work[0].data_ptr<float>(), work[1].data_ptr<float>(), partial.data_ptr<float>(), P,
+            work[2].data_ptr<float>(), work[3].data_ptr<float>(), work[4].data_ptr<float>(),
+            cur_stream());
+  at::Tensor dg, db;
+  if (need_affine_grad) {
+    dg = work[0];
+    db = work[1];
+  }
+  return {dx, dg, db, dz};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -248,4 +361,7 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("lars_step", &lars_step, "fused segmented LARS step");
   m.def("seg_dot3", &seg_dot3, "per-segment (a.b, |a|^2, |b|^2)");
   m.def("adasum_combine", &adasum_combine, "per-segment Adasum merge a <- ca*a + cb*b");
+  m.def("bn_fwd_train", &bn_fwd_train, "fused NHWC BN(+add)(+ReLU) training forward");
+  m.def("bn_apply", &bn_apply, "NHWC y = act(x*scale + bias (+res))");
+  m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward");
 }

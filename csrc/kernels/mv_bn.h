@@ -1,0 +1,22 @@
+// Host launchers for the fused NHWC BatchNorm(+add)(+ReLU) kernels (mv_bn.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// number of row-partials the reduction passes produce (size the [P][2][C] workspace)
+int mv_bn_partials(int64_t M, int C);
+
+void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, float* rmean,
+                     float* rvar, const float* gamma, const float* beta, float momentum, float eps,
+                     bool relu, float* partial, int P, float* save_mean, float* save_invstd,
+                     float* scale, float* bias, hipStream_t st);
+
+void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
+                 const float* bias, bool relu, hipStream_t st);
+
+// mode 0: plain BN, 1: BN+ReLU (mask from x), 2: BN+add+ReLU (mask from y, writes dz)
+void mv_bn_bwd(int mode, const void* dy, const void* x, const void* y, void* dz, void* dx,
+               int64_t M, int C, const float* save_mean, const float* save_invstd,
+               const float* gamma, const float* scale, const float* bias, float* dgamma,
+               float* dbeta, float* partial, int P, float* ca, float* cb, float* cc,
+               hipStream_t st);

@@ -1,0 +1,468 @@
+// Fused NHWC BatchNorm (+ residual add) (+ ReLU) for bf16 activations on gfx950.
+//
+// Why: on ResNet-50 bf16 (bs 256, 1x MI355X) MIOpen's BatchNorm kernels plus the
+// separate ReLU / residual-add / threshold-backward elementwise kernels took
+// ~22 of 39 ms per step at ~3 TB/s (profiles/r1_resnet50_bs256_baseline_miopen_bn.md).
+// Fusing them cuts HBM passes per BN layer from 5 to 3 (fwd, ReLU) / 8 to 4 (fwd,
+// add+ReLU) and from 8 to 5 (bwd, ReLU) / 8 to 7 (bwd, add+ReLU), and every
+// pass streams 16-byte lanes.
+//
+// Layout: x is [M, C] (channels_last, M = N*H*W), C % 8 == 0.  A workgroup owns
+// a slab of CB = min(C, 256) channels (blockIdx.y) and a range of rows
+// (blockIdx.x); each lane owns 8 consecutive channels of one row per step, so
+// the per-channel coefficients stay in registers for the whole slab.
+//
+// Statistics are reduced deterministically (fixed-order block partials, then a
+// fixed-order finalize) so every DP rank computes bit-identical results.
+// Sums are taken around a per-channel shift (the running mean) to limit
+// cancellation in E[x^2] - E[x]^2.
+#include "mv_common.h"
+#include "mv_bn.h"
+
+namespace mv {
+namespace bn {
+
+constexpr int kCB = 256;    // channels per workgroup slab
+constexpr int kTPR = kCB / kVec;  // 32 lanes per row (when C >= 256)
+constexpr int kFinCh = 8;   // finalize: channels per workgroup
+constexpr int kFinSub = kBlock / kFinCh;  // 32 partial-subsets per channel
+
+struct Geo {
+  int64_t M;
+  int C;
+  int CB;    // channels in this launch's slab width (<= kCB)
+  int TPR;   // lanes per row
+  int RPI;   // rows per iteration (per workgroup)
+  int64_t RB;  // rows per workgroup
+};
+
+__device__ __forceinline__ void lane_map(const Geo& g, int* tc, int* tr, int* c, bool* valid) {
+  *tc = threadIdx.x % g.TPR;
+  *tr = threadIdx.x / g.TPR;
+  *c = blockIdx.y * g.CB + *tc * kVec;
+  *valid = (*tr < g.RPI) && (*c < g.C);
+}
+
+__device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = p[j];
+}
+
+// ---------------------------------------------------------------- forward
+__global__ __launch_bounds__(kBlock) void stats_kernel(const __bf16* __restrict__ x,
+                                                        const float* __restrict__ shift,
+                                                        float* __restrict__ partial, Geo g) {
+  int tc, tr, c;
+  bool valid;
+  lane_map(g, &tc, &tr, &c, &valid);
+  float s1[8], s2[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; sh[j] = 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * g.RB;
+  const int64_t r1 = (r0 + g.RB < g.M) ? r0 + g.RB : g.M;
+  if (valid) {
+    if (shift) load8f(shift + c, sh);
+    int64_t r = r0 + tr;
+    for (; r + 3 * g.RPI < r1; r += 4 * g.RPI) {
+      float v0[8], v1[8], v2[8], v3[8];
+      load8(x + r * g.C + c, v0);
+      load8(x + (r + g.RPI) * g.C + c, v1);
+      load8(x + (r + 2 * g.RPI) * g.C + c, v2);
+      load8(x + (r + 3 * g.RPI) * g.C + c, v3);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = v0[j] - sh[j], b = v1[j] - sh[j], cc = v2[j] - sh[j], d = v3[j] - sh[j];
+        s1[j] += (a + b) + (cc + d);
+        s2[j] += (a * a + b * b) + (cc * cc + d * d);
+      }
+    }
+    for (; r < r1; r += g.RPI) {
+      float v0[8];
+      load8(x + r * g.C + c, v0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = v0[j] - sh[j];
+        s1[j] += a;
+        s2[j] += a * a;
+      }
+    }
+  }
+  __shared__ float red[2][kBlock * kVec];   // [k][tr * CB + tc*8 + j]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x * kVec + j] = s1[j];
+    red[1][threadIdx.x * kVec + j] = s2[j];
+  }
+  __syncthreads();
+  const int cb_eff = min(g.CB, g.C - (int)blockIdx.y * g.CB);
+  for (int v = threadIdx.x; v < 2 * cb_eff; v += kBlock) {
+    const int k = v / cb_eff, cc = v % cb_eff;
+    float s = 0.f;
+    for (int t = 0; t < g.RPI; ++t) s += red[k][t * g.TPR * kVec + cc];
+    partial[((int64_t)blockIdx.x * 2 + k) * g.C + blockIdx.y * g.CB + cc] = s;
+  }
+}
+
+// Fixed-order reduction of [P][2][C] partials for kFinCh channels per block.
+__device__ __forceinline__ void fin_reduce(const float* __restrict__ partial, int P, int C, int ch,
+                                           float* o1, float* o2) {
+  __shared__ float red[2][kFinSub][kFinCh];
+  const int lc = threadIdx.x % kFinCh, sub = threadIdx.x / kFinCh;
+  float a = 0.f, b = 0.f;
+  if (ch < C) {
+    for (int p = sub; p < P; p += kFinSub) {
+      a += partial[((int64_t)p * 2) * C + ch];
+      b += partial[((int64_t)p * 2 + 1) * C + ch];
+    }
+  }
+  red[0][sub][lc] = a;
+  red[1][sub][lc] = b;
+  __syncthreads();
+  if (sub == 0) {
+    float x = 0.f, y = 0.f;
+    for (int s = 0; s < kFinSub; ++s) { x += red[0][s][lc]; y += red[1][s][lc]; }
+    *o1 = x;
+    *o2 = y;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void finalize_fwd_kernel(
+    const float* __restrict__ partial, int P, int64_t M, int C, float* __restrict__ rmean,
+    float* __restrict__ rvar, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float momentum, float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
+    float* __restrict__ scale, float* __restrict__ bias) {
+  const int ch = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  float s1 = 0.f, s2 = 0.f;
+  fin_reduce(partial, P, C, ch, &s1, &s2);
+  if (threadIdx.x / kFinCh != 0 || ch >= C) return;
+  const float inv_m = 1.f / (float)M;
+  const float sh = rmean ? rmean[ch] : 0.f;
+  const float ms = s1 * inv_m;
+  float var = fmaxf(s2 * inv_m - ms * ms, 0.f);
+  const float mean = sh + ms;
+  const float invstd = 1.f / sqrtf(var + eps);
+  save_mean[ch] = mean;
+  save_invstd[ch] = invstd;
+  if (rmean) {
+    const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    rmean[ch] = (1.f - momentum) * sh + momentum * mean;
+    rvar[ch] = (1.f - momentum) * rvar[ch] + momentum * unb;
+  }
+  const float sc = (gamma ? gamma[ch] : 1.f) * invstd;
+  scale[ch] = sc;
+  bias[ch] = (beta ? beta[ch] : 0.f) - mean * sc;
+}
+
+template <bool RELU, bool RES>
+__global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict__ x,
+                                                        const __bf16* __restrict__ res,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ bias,
+                                                        __bf16* __restrict__ y, Geo g) {
+  int tc, tr, c;
+  bool valid;
+  lane_map(g, &tc, &tr, &c, &valid);
+  if (!valid) return;
+  float sc[8], bi[8];
+  load8f(scale + c, sc);
+  load8f(bias + c, bi);
+  const int64_t r0 = (int64_t)blockIdx.x * g.RB;
+  const int64_t r1 = (r0 + g.RB < g.M) ? r0 + g.RB : g.M;
+  int64_t r = r0 + tr;
+  for (; r + g.RPI < r1; r += 2 * g.RPI) {
+    float v0[8], v1[8], q0[8], q1[8];
+    const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
+    load8(x + o0, v0);
+    load8(x + o1, v1);
+    if (RES) { load8(res + o0, q0); load8(res + o1, q1); }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = __builtin_fmaf(v0[j], sc[j], bi[j]);
+      float b = __builtin_fmaf(v1[j], sc[j], bi[j]);
+      if (RES) { a += q0[j]; b += q1[j]; }
+      if (RELU) { a = fmaxf(a, 0.f); b = fmaxf(b, 0.f); }
+      v0[j] = a;
+      v1[j] = b;
+    }
+    store8(y + o0, v0);
+    store8(y + o1, v1);
+  }
+  for (; r < r1; r += g.RPI) {
+    float v0[8], q0[8];
+    const int64_t o0 = r * g.C + c;
+    load8(x + o0, v0);
+    if (RES) load8(res + o0, q0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = __builtin_fmaf(v0[j], sc[j], bi[j]);
+      if (RES) a += q0[j];
+      if (RELU) a = fmaxf(a, 0.f);
+      v0[j] = a;
+    }
+    store8(y + o0, v0);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// MODE 0: no activation (d = dy)
+// MODE 1: ReLU, mask recomputed from x:  d = (fma(x, scale, bias) > 0) ? dy : 0
+// MODE 2: add + ReLU, mask from the saved output y: d = (y > 0) ? dy : 0; d is
+//         written out (it is also the residual branch's gradient)
+template <int MODE>
+__device__ __forceinline__ void masked(const float (&dy)[8], const float (&x)[8],
+                                       const float (&yv)[8], const float (&sc)[8],
+                                       const float (&bi)[8], float (&d)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (MODE == 0) d[j] = dy[j];
+    else if (MODE == 1) d[j] = __builtin_fmaf(x[j], sc[j], bi[j]) > 0.f ? dy[j] : 0.f;
+    else d[j] = yv[j] > 0.f ? dy[j] : 0.f;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
+    const __bf16* __restrict__ dy, const __bf16* __restrict__ x, const __bf16* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ scale,
+    const float* __restrict__ bias, __bf16* __restrict__ dz, float* __restrict__ partial, Geo g) {
+  int tc, tr, c;
+  bool valid;
+  lane_map(g, &tc, &tr, &c, &valid);
+  float s1[8], s2[8], mu[8], sc[8], bi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; mu[j] = 0.f; sc[j] = 0.f; bi[j] = 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * g.RB;
+  const int64_t r1 = (r0 + g.RB < g.M) ? r0 + g.RB : g.M;
+  if (valid) {
+    load8f(mean + c, mu);
+    if (MODE == 1) { load8f(scale + c, sc); load8f(bias + c, bi); }
+    int64_t r = r0 + tr;
+    for (; r + g.RPI < r1; r += 2 * g.RPI) {
+      float a0[8], a1[8], x0[8], x1[8], y0[8], y1[8], d0[8], d1[8];
+      const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
+      load8(dy + o0, a0);
+      load8(dy + o1, a1);
+      load8(x + o0, x0);
+      load8(x + o1, x1);
+      if (MODE == 2) { load8(y + o0, y0); load8(y + o1, y1); }
+      masked<MODE>(a0, x0, y0, sc, bi, d0);
+      masked<MODE>(a1, x1, y1, sc, bi, d1);
+      if (MODE == 2) { store8(dz + o0, d0); store8(dz + o1, d1); }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += d0[j] + d1[j];
+        s2[j] += d0[j] * (x0[j] - mu[j]) + d1[j] * (x1[j] - mu[j]);
+      }
+    }
+    for (; r < r1; r += g.RPI) {
+      float a0[8], x0[8], y0[8], d0[8];
+      const int64_t o0 = r * g.C + c;
+      load8(dy + o0, a0);
+      load8(x + o0, x0);
+      if (MODE == 2) load8(y + o0, y0);
+      masked<MODE>(a0, x0, y0, sc, bi, d0);
+      if (MODE == 2) store8(dz + o0, d0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += d0[j];
+        s2[j] += d0[j] * (x0[j] - mu[j]);
+      }
+    }
+  }
+  __shared__ float red[2][kBlock * kVec];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x * kVec + j] = s1[j];
+    red[1][threadIdx.x * kVec + j] = s2[j];
+  }
+  __syncthreads();
+  const int cb_eff = min(g.CB, g.C - (int)blockIdx.y * g.CB);
+  for (int v = threadIdx.x; v < 2 * cb_eff; v += kBlock) {
+    const int k = v / cb_eff, cc = v % cb_eff;
+    float s = 0.f;
+    for (int t = 0; t < g.RPI; ++t) s += red[k][t * g.TPR * kVec + cc];
+    partial[((int64_t)blockIdx.x * 2 + k) * g.C + blockIdx.y * g.CB + cc] = s;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void finalize_bwd_kernel(
+    const float* __restrict__ partial, int P, int64_t M, int C, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ ca,
+    float* __restrict__ cb, float* __restrict__ cc) {
+  const int ch = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  float sdz = 0.f, sdzx = 0.f;
+  fin_reduce(partial, P, C, ch, &sdz, &sdzx);
+  if (threadIdx.x / kFinCh != 0 || ch >= C) return;
+  const float is = invstd[ch];
+  if (dgamma) dgamma[ch] = sdzx * is;
+  if (dbeta) dbeta[ch] = sdz;
+  const float gm = gamma ? gamma[ch] : 1.f;
+  const float inv_m = 1.f / (float)M;
+  const float a = gm * is;
+  const float b = -a * is * is * sdzx * inv_m;
+  ca[ch] = a;
+  cb[ch] = b;
+  cc[ch] = -a * sdz * inv_m - b * mean[ch];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void bwd_dx_kernel(
+    const __bf16* __restrict__ d_in, const __bf16* __restrict__ x,
+    const float* __restrict__ scale, const float* __restrict__ bias, const float* __restrict__ ca,
+    const float* __restrict__ cb, const float* __restrict__ cc, __bf16* __restrict__ dx, Geo g) {
+  int tc, tr, c;
+  bool valid;
+  lane_map(g, &tc, &tr, &c, &valid);
+  if (!valid) return;
+  float a[8], b[8], k[8], sc[8], bi[8];
+  load8f(ca + c, a);
+  load8f(cb + c, b);
+  load8f(cc + c, k);
+  if (MODE == 1) { load8f(scale + c, sc); load8f(bias + c, bi); }
+  const int64_t r0 = (int64_t)blockIdx.x * g.RB;
+  const int64_t r1 = (r0 + g.RB < g.M) ? r0 + g.RB : g.M;
+  int64_t r = r0 + tr;
+  for (; r + g.RPI < r1; r += 2 * g.RPI) {
+    float d0[8], d1[8], x0[8], x1[8];
+    const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
+    load8(d_in + o0, d0);
+    load8(d_in + o1, d1);
+    load8(x + o0, x0);
+    load8(x + o1, x1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float e0 = d0[j], e1 = d1[j];
+      if (MODE == 1) {
+        e0 = __builtin_fmaf(x0[j], sc[j], bi[j]) > 0.f ? e0 : 0.f;
+        e1 = __builtin_fmaf(x1[j], sc[j], bi[j]) > 0.f ? e1 : 0.f;
+      }
+      d0[j] = a[j] * e0 + (b[j] * x0[j] + k[j]);
+      d1[j] = a[j] * e1 + (b[j] * x1[j] + k[j]);
+    }
+    store8(dx + o0, d0);
+    store8(dx + o1, d1);
+  }
+  for (; r < r1; r += g.RPI) {
+    float d0[8], x0[8];
+    const int64_t o0 = r * g.C + c;
+    load8(d_in + o0, d0);
+    load8(x + o0, x0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float e0 = d0[j];
+      if (MODE == 1) e0 = __builtin_fmaf(x0[j], sc[j], bi[j]) > 0.f ? e0 : 0.f;
+      d0[j] = a[j] * e0 + (b[j] * x0[j] + k[j]);
+    }
+    store8(dx + o0, d0);
+  }
+}
+
+static Geo make_geo(int64_t M, int C, int64_t rows_per_block) {
+  Geo g;
+  g.M = M;
+  g.C = C;
+  g.CB = C < kCB ? C : kCB;
+  g.TPR = g.CB / kVec;
+  g.RPI = kBlock / g.TPR;
+  int64_t rb = rows_per_block;
+  if (rb < g.RPI) rb = g.RPI;
+  rb = (rb + g.RPI - 1) / g.RPI * g.RPI;
+  g.RB = rb;
+  return g;
+}
+
+static dim3 grid_of(const Geo& g) {
+  const int64_t gx = (g.M + g.RB - 1) / g.RB;
+  const int gy = (g.C + g.CB - 1) / g.CB;
+  return dim3((unsigned)gx, (unsigned)gy);
+}
+
+}  // namespace bn
+}  // namespace mv
+
+using namespace mv;
+using namespace mv::bn;
+
+// Rows per workgroup for the reduction passes: >= 128 rows and <= 2048 row
+// blocks in total, which keeps the [P][2][C] partials a few % of the input.
+int mv_bn_partials(int64_t M, int C) {
+  Geo g = make_geo(M, C, 128);
+  const int gy = (C + g.CB - 1) / g.CB;
+  int64_t p = (M + 127) / 128;
+  const int64_t cap = 2048 / gy > 0 ? 2048 / gy : 1;
+  if (p > cap) p = cap;
+  if (p < 1) p = 1;
+  return (int)p;
+}
+
+static Geo reduce_geo(int64_t M, int C, int P) {
+  return make_geo(M, C, (M + P - 1) / P);
+}
+
+static Geo apply_geo(int64_t M, int C) {
+  Geo g0 = make_geo(M, C, 64);
+  const int gy = (C + g0.CB - 1) / g0.CB;
+  int64_t blocks = (M + 63) / 64;
+  const int64_t cap = 4096 / gy > 0 ? 4096 / gy : 1;
+  if (blocks > cap) blocks = cap;
+  return make_geo(M, C, (M + blocks - 1) / blocks);
+}
+
+void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, float* rmean,
+                     float* rvar, const float* gamma, const float* beta, float momentum, float eps,
+                     bool relu, float* partial, int P, float* save_mean, float* save_invstd,
+                     float* scale, float* bias, hipStream_t st) {
+  Geo gr = reduce_geo(M, C, P);
+  dim3 grr = grid_of(gr);
+  hipLaunchKernelGGL(stats_kernel, grr, dim3(kBlock), 0, st, (const __bf16*)x, rmean, partial, gr);
+  hipLaunchKernelGGL(finalize_fwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
+                     partial, (int)grr.x, M, C, rmean, rvar, gamma, beta, momentum, eps, save_mean,
+                     save_invstd, scale, bias);
+  mv_bn_apply(x, res, y, M, C, scale, bias, relu, st);
+}
+
+void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
+                 const float* bias, bool relu, hipStream_t st) {
+  Geo ga = apply_geo(M, C);
+  dim3 gg = grid_of(ga);
+  const __bf16* xp = (const __bf16*)x;
+  const __bf16* rp = (const __bf16*)res;
+  __bf16* yp = (__bf16*)y;
+  if (res) {
+    if (relu) hipLaunchKernelGGL((apply_kernel<true, true>), gg, dim3(kBlock), 0, st, xp, rp, scale, bias, yp, ga);
+    else hipLaunchKernelGGL((apply_kernel<false, true>), gg, dim3(kBlock), 0, st, xp, rp, scale, bias, yp, ga);
+  } else {
+    if (relu) hipLaunchKernelGGL((apply_kernel<true, false>), gg, dim3(kBlock), 0, st, xp, rp, scale, bias, yp, ga);
+    else hipLaunchKernelGGL((apply_kernel<false, false>), gg, dim3(kBlock), 0, st, xp, rp, scale, bias, yp, ga);
+  }
+}
+
+void mv_bn_bwd(int mode, const void* dy, const void* x, const void* y, void* dz, void* dx,
+               int64_t M, int C, const float* save_mean, const float* save_invstd,
+               const float* gamma, const float* scale, const float* bias, float* dgamma,
+               float* dbeta, float* partial, int P, float* ca, float* cb, float* cc,
+               hipStream_t st) {
+  Geo gr = reduce_geo(M, C, P);
+  dim3 grr = grid_of(gr);
+  const __bf16* dyp = (const __bf16*)dy;
+  const __bf16* xp = (const __bf16*)x;
+  const __bf16* yp = (const __bf16*)y;
+  __bf16* dzp = (__bf16*)dz;
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((bwd_reduce_kernel<0>), grr, dim3(kBlock), 0, st, dyp, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
+    case 1: hipLaunchKernelGGL((bwd_reduce_kernel<1>), grr, dim3(kBlock), 0, st, dyp, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
+    default: hipLaunchKernelGGL((bwd_reduce_kernel<2>), grr, dim3(kBlock), 0, st, dyp, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
+  }
+  hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
+                     partial, (int)grr.x, M, C, save_mean, save_invstd, gamma, dgamma, dbeta, ca,
+                     cb, cc);
+  Geo ga = apply_geo(M, C);
+  dim3 gg = grid_of(ga);
+  __bf16* dxp = (__bf16*)dx;
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((bwd_dx_kernel<0>), gg, dim3(kBlock), 0, st, dyp, xp, scale, bias, ca, cb, cc, dxp, ga); break;
+    case 1: hipLaunchKernelGGL((bwd_dx_kernel<1>), gg, dim3(kBlock), 0, st, dyp, xp, scale, bias, ca, cb, cc, dxp, ga); break;
+    default: hipLaunchKernelGGL((bwd_dx_kernel<0>), gg, dim3(kBlock), 0, st, (const __bf16*)dzp, xp, scale, bias, ca, cb, cc, dxp, ga); break;
+  }
+}

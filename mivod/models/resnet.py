@@ -12,6 +12,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.bn import BatchNorm2d
+
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=dilation, groups=groups, bias=False,
@@ -28,25 +30,21 @@ class Bottleneck(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None, zero_init_residual=False):
         super().__init__()
         self.conv1 = conv1x1(inplanes, planes)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = BatchNorm2d(planes)
         self.conv2 = conv3x3(planes, planes, stride)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = BatchNorm2d(planes)
         self.conv3 = conv1x1(planes, planes * self.expansion)
-        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.bn3 = BatchNorm2d(planes * self.expansion)
         if zero_init_residual:
             nn.init.zeros_(self.bn3.weight)
-        self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        if self.downsample is not None:
-            identity = self.downsample(x)
-        out += identity
-        return self.relu(out)
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x), relu=True)
+        out = self.bn2(self.conv2(out), relu=True)
+        # fused: relu(bn3(conv3(out)) + identity) in one pass (mivod.ops.bn)
+        return self.bn3(self.conv3(out), residual=identity, relu=True)
 
 
 class ResNet(nn.Module):
@@ -54,8 +52,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BatchNorm2d(64)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(64, layers[0], 1, zero_init_residual)
         self.layer2 = self._make_layer(128, layers[1], 2, zero_init_residual)
@@ -74,7 +71,7 @@ class ResNet(nn.Module):
         down = None
         if stride != 1 or self.inplanes != planes * Bottleneck.expansion:
             down = nn.Sequential(conv1x1(self.inplanes, planes * Bottleneck.expansion, stride),
-                                 nn.BatchNorm2d(planes * Bottleneck.expansion))
+                                 BatchNorm2d(planes * Bottleneck.expansion))
         layers = [Bottleneck(self.inplanes, planes, stride, down, zir)]
         self.inplanes = planes * Bottleneck.expansion
         for _ in range(1, blocks):
@@ -82,7 +79,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x), relu=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
