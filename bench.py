@@ -23,6 +23,22 @@ import sys
 import time
 
 os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+# Ship MIOpen's find-db + compiled-kernel cache with the repo (.miopen/): a fresh
+# MI355X box otherwise spends ~3 minutes JIT-compiling ResNet-50's conv kernels.
+_MIO = os.path.join(os.path.dirname(os.path.abspath(__file__)), ".miopen")
+if os.path.isdir(_MIO) and "MIOPEN_USER_DB_PATH" not in os.environ:
+    import shutil
+    import tempfile
+    _tmp = os.path.join(tempfile.gettempdir(), f"mivod_miopen_{os.getuid()}")
+    for sub, var in (("db", "MIOPEN_USER_DB_PATH"), ("cache", "MIOPEN_CUSTOM_CACHE_DIR")):
+        dst = os.path.join(_tmp, sub)
+        os.makedirs(dst, exist_ok=True)
+        src = os.path.join(_MIO, sub)
+        if os.path.isdir(src):
+            for f in os.listdir(src):
+                if not os.path.exists(os.path.join(dst, f)):
+                    shutil.copy2(os.path.join(src, f), os.path.join(dst, f))
+        os.environ.setdefault(var, dst)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 BASELINE_METRIC = "images/sec (whole node) + scaling efficiency, ResNet-50 bf16 at 1/2/4/8 MI355X"

@@ -24,8 +24,8 @@ namespace bn {
 
 constexpr int kCB = 256;    // channels per workgroup slab
 constexpr int kTPR = kCB / kVec;  // 32 lanes per row (when C >= 256)
-constexpr int kFinCh = 8;   // finalize: channels per workgroup
-constexpr int kFinSub = kBlock / kFinCh;  // 32 partial-subsets per channel
+constexpr int kFinCh = 2;   // finalize: channels per workgroup
+constexpr int kFinSub = kBlock / kFinCh;  // 128 partial-subsets per channel
 
 struct Geo {
   int64_t M;
@@ -106,21 +106,48 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(const __bf16* __restrict_
 // Fixed-order reduction of [P][2][C] partials for kFinCh channels per block.
 __device__ __forceinline__ void fin_reduce(const float* __restrict__ partial, int P, int C, int ch,
                                            float* o1, float* o2) {
-  __shared__ float red[2][kFinSub][kFinCh];
   const int lc = threadIdx.x % kFinCh, sub = threadIdx.x / kFinCh;
-  float a = 0.f, b = 0.f;
+  // 4 independent accumulator pairs keep 8 loads in flight per lane; the
+  // combination order is fixed, so the result is deterministic.
+  float a0 = 0.f, b0 = 0.f, a1 = 0.f, b1 = 0.f, a2 = 0.f, b2 = 0.f, a3 = 0.f, b3 = 0.f;
   if (ch < C) {
-    for (int p = sub; p < P; p += kFinSub) {
-      a += partial[((int64_t)p * 2) * C + ch];
-      b += partial[((int64_t)p * 2 + 1) * C + ch];
+    const int64_t st = (int64_t)2 * C;
+    const float* q = partial + ch;
+    int p = sub;
+    for (; p + 3 * kFinSub < P; p += 4 * kFinSub) {
+      a0 += q[(int64_t)p * st];
+      b0 += q[(int64_t)p * st + C];
+      a1 += q[(int64_t)(p + kFinSub) * st];
+      b1 += q[(int64_t)(p + kFinSub) * st + C];
+      a2 += q[(int64_t)(p + 2 * kFinSub) * st];
+      b2 += q[(int64_t)(p + 2 * kFinSub) * st + C];
+      a3 += q[(int64_t)(p + 3 * kFinSub) * st];
+      b3 += q[(int64_t)(p + 3 * kFinSub) * st + C];
+    }
+    for (; p < P; p += kFinSub) {
+      a0 += q[(int64_t)p * st];
+      b0 += q[(int64_t)p * st + C];
     }
   }
-  red[0][sub][lc] = a;
-  red[1][sub][lc] = b;
+  float a = (a0 + a1) + (a2 + a3), b = (b0 + b1) + (b2 + b3);
+  // fixed xor-tree across the 32 lanes of a wave that share this channel
+  // (lane = sub*kFinCh + lc), then 4 wave partials combined in order via LDS
+#pragma unroll
+  for (int o = kFinCh; o < kWave; o <<= 1) {
+    a += __shfl_xor(a, o, kWave);
+    b += __shfl_xor(b, o, kWave);
+  }
+  __shared__ float red[2][kBlock / kWave][kFinCh];
+  const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  if (lane < kFinCh) {
+    red[0][w][lane] = a;
+    red[1][w][lane] = b;
+  }
   __syncthreads();
   if (sub == 0) {
     float x = 0.f, y = 0.f;
-    for (int s = 0; s < kFinSub; ++s) { x += red[0][s][lc]; y += red[1][s][lc]; }
+#pragma unroll
+    for (int k = 0; k < kBlock / kWave; ++k) { x += red[0][k][lc]; y += red[1][k][lc]; }
     *o1 = x;
     *o2 = y;
   }

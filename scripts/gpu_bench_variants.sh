@@ -1,0 +1,29 @@
+#!/bin/bash
+# Bench variants in one GPU session (MIOpen cache shared across steps).
+set -u
+mkdir -p gpurun_out
+export MIOPEN_USER_DB_PATH=$PWD/gpurun_out/miopen_db
+export MIOPEN_CUSTOM_CACHE_DIR=$PWD/gpurun_out/miopen_cache
+mkdir -p "$MIOPEN_USER_DB_PATH" "$MIOPEN_CUSTOM_CACHE_DIR"
+[ -d .miopen/db ] && cp -rn .miopen/db/. "$MIOPEN_USER_DB_PATH"/ 2>/dev/null
+[ -d .miopen/cache ] && cp -rn .miopen/cache/. "$MIOPEN_CUSTOM_CACHE_DIR"/ 2>/dev/null
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; grep -E '^\{|\[bench\] warmup [0-9]+ steps|passed|failed|Error' "gpurun_out/$name.log" | tail -5
+  if { [ $rc -ge 2 ] && [ $rc -ne 5 ]; }; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+}
+for v in ${VARIANTS:-default}; do
+  case $v in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    default) run bench_default 1200 python bench.py --steps 20 --warmup 10 ;;
+    normal) MIOPEN_FIND_MODE=NORMAL run bench_normal 1200 python bench.py --steps 20 --warmup 10 ;;
+    bs512) run bench_bs512 1200 python bench.py --steps 20 --warmup 10 --batch 512 ;;
+    bs128) run bench_bs128 1200 python bench.py --steps 20 --warmup 10 --batch 128 ;;
+    lars) run bench_lars 1200 python bench.py --steps 20 --warmup 10 --optimizer lars ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+          run rocprof 1200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 5 ${BENCH_ARGS:-} ;;
+  esac
+done

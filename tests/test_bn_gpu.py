@@ -9,7 +9,7 @@ from mivod.ops.bn import BatchNorm2d, batch_norm_act
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(4, 64, 8, 8), (2, 256, 7, 7), (3, 2048, 3, 3), (2, 96, 5, 5), (8, 512, 14, 14),
-          (1, 64, 1, 1)]
+          (2, 64, 1, 1)]
 
 
 def _ref(x, w, b, rm, rv, mom, eps, relu, res):
@@ -38,10 +38,10 @@ def test_bn_fused_train(cuda, shape, relu, use_res):
     rm = torch.randn(C, device=cuda) * 0.1
     rv = torch.rand(C, device=cuda) + 0.5
     rm2, rv2 = rm.clone(), rv.clone()
-    xr = x.detach().clone().requires_grad_()
+    xr = x.detach().float().requires_grad_()
     x1 = x.detach().clone().requires_grad_()
     r1 = res.detach().clone().requires_grad_() if use_res else None
-    rr = res.detach().clone().requires_grad_() if use_res else None
+    rr = res.detach().float().requires_grad_() if use_res else None
     w2 = w.detach().clone().requires_grad_()
     b2 = b.detach().clone().requires_grad_()
 
