@@ -1,0 +1,82 @@
+"""Launcher (mivodrun / horovodrun parity) — CPU tier."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from mivod.run.launcher import (assign_slots, build_parser, exported_env, parse_hostfile,
+                                parse_hosts, tuning_env)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_parse_hosts_and_hostfile(tmp_path):
+    assert parse_hosts("a:4,b:2,c") == [("a", 4), ("b", 2), ("c", 1)]
+    hf = tmp_path / "hostfile"
+    hf.write_text("# comment\nnode1 slots=4\nnode2:2\nnode3\n")
+    assert parse_hostfile(str(hf)) == [("node1", 4), ("node2", 2), ("node3", 1)]
+
+
+def test_assign_slots_topology():
+    s = assign_slots([("a", 2), ("b", 2)], 4)
+    assert [(x.host, x.rank, x.local_rank, x.local_size) for x in s] == [
+        ("a", 0, 0, 2), ("a", 1, 1, 2), ("b", 2, 0, 2), ("b", 3, 1, 2)]
+    assert [(x.cross_rank, x.cross_size) for x in s] == [(0, 2), (0, 2), (1, 2), (1, 2)]
+    with pytest.raises(ValueError):
+        assign_slots([("a", 1)], 2)
+
+
+def test_mpirun_flags_tolerated_and_tuning_mapped():
+    # the reference's mpirun line (README.md:57) with mpirun -> mivodrun
+    argv = ("--allow-run-as-root -np 1 --hostfile /generated/hostfile -bind-to none -map-by slot "
+            "-x NCCL_DEBUG=INFO -mca pml ob1 -mca btl ^openib --fusion-threshold-mb 32 "
+            "--cycle-time-ms 2 --timeline-filename /tmp/tl.json --no-stall-check "
+            "python keras_mnist.py --epochs 1").split()
+    a = build_parser().parse_args(argv)
+    assert a.np == 1 and a.hostfile == "/generated/hostfile"
+    assert a.command == ["python", "keras_mnist.py", "--epochs", "1"]
+    env = tuning_env(a)
+    assert env["HOROVOD_FUSION_THRESHOLD"] == str(32 * 2 ** 20)
+    assert env["HOROVOD_CYCLE_TIME"] == "2"
+    assert env["HOROVOD_TIMELINE"] == "/tmp/tl.json"
+    assert env["HOROVOD_STALL_CHECK_DISABLE"] == "1"
+    assert exported_env(a.export) == {"NCCL_DEBUG": "INFO"}
+
+
+SCRIPT = r'''
+import os, sys
+sys.path.insert(0, %r)
+import torch
+import mivod as hvd
+hvd.init()
+x = hvd.allreduce(torch.tensor([float(hvd.rank())]), op=hvd.Sum)
+print("rank", hvd.rank(), "size", hvd.size(), "local", hvd.local_rank(), "sum", float(x),
+      "nccl_debug", os.environ.get("NCCL_DEBUG"))
+hvd.shutdown()
+''' % ROOT
+
+
+def test_launch_two_local_ranks(tmp_path):
+    f = tmp_path / "prog.py"
+    f.write_text(SCRIPT)
+    env = dict(os.environ, MIVOD_TRANSPORT="gloo", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "mivod.run", "-np", "2", "-H", "localhost:2",
+                        "-x", "NCCL_DEBUG=INFO", "python", str(f)], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "[0]<stdout>:rank 0 size 2 local 0 sum 1.0 nccl_debug INFO" in r.stdout, r.stdout
+    assert "[1]<stdout>:rank 1 size 2 local 1 sum 1.0 nccl_debug INFO" in r.stdout, r.stdout
+
+
+def test_launch_failure_kills_all(tmp_path):
+    f = tmp_path / "fail.py"
+    f.write_text("import os, time, sys\n"
+                 "r = int(os.environ['HOROVOD_RANK'])\n"
+                 "time.sleep(0.5)\n"
+                 "sys.exit(3) if r == 1 else time.sleep(120)\n")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bin", "horovodrun"), "-np", "2",
+                        sys.executable, str(f)], cwd=ROOT, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 3, r.stdout + r.stderr
+    assert "rank 1 exited with code 3" in r.stderr
