@@ -237,8 +237,8 @@ __global__ __launch_bounds__(kBlock) void adam_flat_kernel(const TG* __restrict_
       mv_[j] = hp.b1 * mv_[j] + (1.f - hp.b1) * gr;
       vv[j] = hp.b2 * vv[j] + (1.f - hp.b2) * gr * gr;
       if (hp.adamw) wv[j] *= (1.f - hp.lr * hp.wd);
-      float denom = hp.keras_eps ? (sqrtf(vv[j]) + hp.eps * sqrtf(hp.bc2)) * rbc2
-                                 : sqrtf(vv[j]) * rbc2 + hp.eps;
+      // torch: m_hat / (sqrt(v_hat) + eps); Keras/TF: lr*sqrt(bc2)/bc1 * m / (sqrt(v) + eps)
+      float denom = hp.keras_eps ? (sqrtf(vv[j]) + hp.eps) * rbc2 : sqrtf(vv[j]) * rbc2 + hp.eps;
       wv[j] -= step * mv_[j] / denom;
     }
     if (cnt == kVec) {

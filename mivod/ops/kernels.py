@@ -151,7 +151,7 @@ def adam_step(g, w, m, v, model, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight
     if adamw and weight_decay:
         w.mul_(1 - lr * weight_decay)
     if keras_eps:
-        denom = (v.sqrt() + eps * math.sqrt(bc2)) / math.sqrt(bc2)
+        denom = (v.sqrt() + eps) / math.sqrt(bc2)
     else:
         denom = v.sqrt() / math.sqrt(bc2) + eps
     w.addcdiv_(m, denom, value=-lr / bc1)

@@ -298,6 +298,26 @@ def timeline():
     print("OK", hvd_rank())
 
 
+def keras_tf2():
+    """Config 2 (TF2-style Keras MNIST, 2 ranks): broadcast at batch 0, averaged
+    gradients, MetricAverageCallback, LR warmup -> identical weights and logs."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "examples"))
+    os.environ["PS_MODEL_PATH"] = tempfile.mkdtemp()
+    from keras_mnist_tf2_style import main
+    hist, model = main(["--epochs", "4", "--steps", "15"])
+    r = hvd.rank()
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    allf = hvd.allgather(flat.unsqueeze(0))
+    assert torch.equal(allf[0], allf[1])
+    logs = hvd.allgather_object(hist.history)
+    assert logs[0]["loss"] == logs[1]["loss"], logs       # averaged in place, identical
+    assert logs[0]["loss"][-1] < logs[0]["loss"][0], logs[0]["loss"]
+    assert abs(logs[0]["lr"][-1] - 0.001 * hvd.size()) < 1e-9, logs[0]["lr"]
+    hvd.shutdown()
+    print("OK", r)
+
+
 def hvd_rank():
     return int(os.environ.get("RANK", "0"))
 

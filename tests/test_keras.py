@@ -1,0 +1,172 @@
+"""Keras front end + horovod Keras API (CPU tier).
+
+Pins the behavioural contracts of SURVEY.md §8.2: ConvNet parity (1,199,882
+params), the reference CI loss gate (mean loss in 0.0..0.3,
+/root/reference/.ps_project/config.yaml:8-11) on a truncated config-1 run,
+rank-0 checkpoint/TensorBoard/export artefacts, LR warmup closed form,
+DistributedOptimizer class-name preservation, hvd.load_model re-wrapping."""
+import glob
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "examples"))
+
+import mivod.keras as hvd  # noqa: E402
+import mivod.kerasfw as keras  # noqa: E402
+from mivod.kerasfw import backend as K  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _init():
+    hvd.init()
+    yield
+
+
+def test_convnet_parameter_count_and_keras_layouts():
+    from keras_mnist_convnet import build_convnet
+    m = build_convnet((28, 28, 1), 10)
+    assert m.count_params() == 1199882
+    shapes = [w.shape for w in m.get_weights()]
+    assert shapes == [(3, 3, 1, 32), (32,), (3, 3, 32, 64), (64,), (9216, 128), (128,),
+                      (128, 10), (10,)]
+    w = m.get_weights()
+    m.set_weights([x * 2 for x in w])
+    np.testing.assert_allclose(m.get_weights()[4], w[4] * 2, rtol=1e-6)
+
+
+def test_config1_convnet_loss_gate_and_artifacts(tmp_path, monkeypatch):
+    from keras_mnist_convnet import main
+    monkeypatch.setenv("PS_MODEL_PATH", str(tmp_path))
+    hist, score = main(["--epochs", "2", "--train-samples", "16000"])
+    losses = hist.history["loss"]
+    # the reference CI check: aggregate mean of the loss in [0.0, 0.3] — here on the
+    # last epoch of a truncated run (the full 12-epoch run averages far below).
+    assert 0.0 <= losses[-1] <= 0.3, losses
+    assert score[1] > 0.95, score
+    md = tmp_path / "horovod-mnist"
+    assert (md / "checkpoint-1.h5").exists() and (md / "checkpoint-2.h5").exists()
+    assert (md / "keras-sample-model.h5").exists()
+    ev = glob.glob(str(md / "eval" / "train" / "events.out.tfevents.*"))
+    assert ev
+    from mivod.kerasfw.tfevents import read_events
+    recs = read_events(ev[0])
+    assert any("batch_loss" in s for _, s in recs)
+    exports = [d for d in os.listdir(tmp_path) if d[:2] == "20"]
+    assert exports and os.path.exists(tmp_path / exports[0] / "signature.json")
+
+
+def test_save_load_roundtrip_and_hvd_load_model(tmp_path):
+    from keras_mnist_convnet import build_convnet
+    (x, y), _ = keras.datasets.mnist.load_data()
+    x = x[:512].reshape(-1, 28, 28, 1).astype("float32") / 255
+    y = keras.utils.to_categorical(y[:512], 10)
+    m = build_convnet((28, 28, 1), 10)
+    m.compile(loss="categorical_crossentropy",
+              optimizer=hvd.DistributedOptimizer(keras.optimizers.Adadelta(1.0)),
+              metrics=["accuracy"])
+    assert type(m.optimizer).__name__ == "Adadelta"
+    assert isinstance(m.optimizer, keras.optimizers.Adadelta)
+    m.fit(x, y, batch_size=128, epochs=1, verbose=0)
+    p = str(tmp_path / "m.h5")
+    m.save(p)
+    plain = keras.load_model(p)                      # plain loader works (class name kept)
+    np.testing.assert_allclose(plain.predict(x[:16]), m.predict(x[:16]), rtol=1e-5, atol=1e-6)
+    wrapped = hvd.load_model(p)
+    assert type(wrapped.optimizer).__name__ == "Adadelta"
+    assert isinstance(wrapped.optimizer, hvd._DistributedOptimizerMixin)
+    assert wrapped.optimizer.iterations == m.optimizer.iterations
+    # optimizer slots (Adadelta accumulators) restored exactly
+    for pa, pb in zip(m.optimizer._params, wrapped.optimizer._params):
+        sa, sb = m.optimizer._impl.state[pa], wrapped.optimizer._impl.state[pb]
+        for k in ("square_avg", "acc_delta"):
+            torch.testing.assert_close(sb[k], sa[k])
+
+
+def test_lr_warmup_closed_form(monkeypatch, capsys):
+    from mivod.keras import callbacks as hcb
+    n, w, spe, lr0 = 4, 3, 10, 0.004
+    monkeypatch.setattr(hcb.basics, "size", lambda: n)
+    model = keras.Sequential([keras.layers.Dense(2, input_shape=(3,))])
+    model.compile(optimizer=keras.optimizers.SGD(lr=lr0, momentum=0.9), loss="mse")
+    cb = hcb.LearningRateWarmupCallback(warmup_epochs=w, verbose=1, steps_per_epoch=spe)
+    cb.set_model(model)
+    cb.set_params({"steps": spe})
+    cb.on_train_begin()
+    seen = []
+    for epoch in range(w + 1):
+        cb.on_epoch_begin(epoch)
+        for b in range(spe):
+            cb.on_batch_begin(b)
+            seen.append((epoch, b, K.get_value(model.optimizer.lr),
+                         K.get_value(model.optimizer.momentum)))
+            cb.on_batch_end(b)
+            assert abs(K.get_value(model.optimizer.momentum) - 0.9) < 1e-12   # restored
+        logs = {}
+        cb.on_epoch_end(epoch, logs)
+        assert "lr" in logs
+    for epoch, b, lr, _mom in seen:
+        if epoch >= w:
+            continue
+        e = epoch + b / spe + 1 / spe
+        assert math.isclose(lr, lr0 / n * (e * (n - 1) / w + 1), rel_tol=1e-12)
+    last = [s for s in seen if s[0] == w - 1][-1]
+    assert math.isclose(last[2], lr0, rel_tol=1e-12)          # reaches lr0 at warmup end
+    # momentum correction used the lr ratio on the adjusted step
+    assert "finished gradual learning rate warmup to 0.004" in capsys.readouterr().out
+
+
+def test_metric_average_single_rank_noop():
+    from mivod.keras.callbacks import MetricAverageCallback
+    logs = {"loss": 0.5, "accuracy": 0.9}
+    MetricAverageCallback().on_epoch_end(0, logs)
+    assert logs == {"loss": 0.5, "accuracy": 0.9}
+
+
+def test_dataset_pipeline_semantics():
+    x = np.arange(10)
+    y = np.arange(10) * 10
+    ds = keras.data.Dataset.from_tensor_slices((x, y)).batch(4)
+    bs = list(ds)
+    assert [b[0].tolist() for b in bs] == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+    assert len(ds) == 3
+    sh = keras.data.Dataset.from_tensor_slices((x,)).shuffle(4, seed=0)
+    assert sorted(sh) == list(range(10))
+    rep = iter(keras.data.Dataset.from_tensor_slices((x, y)).repeat().shuffle(5).batch(3))
+    seen = [next(rep)[0] for _ in range(7)]
+    assert all(len(s) == 3 for s in seen)
+    vals = np.concatenate(seen)
+    assert set(vals.tolist()) <= set(range(10))
+
+
+def test_tfevents_roundtrip(tmp_path):
+    from mivod.kerasfw.tfevents import EventWriter, crc32c, read_events
+    assert crc32c(b"123456789") == 0xE3069283          # CRC-32C check value
+    w = EventWriter(str(tmp_path))
+    w.add_scalars(5, {"loss": 0.25, "accuracy": 0.5})
+    w.close()
+    recs = read_events(w.path)
+    assert recs[-1][0] == 5 and abs(recs[-1][1]["loss"] - 0.25) < 1e-7
+
+
+def test_keras_adam_matches_closed_form():
+    torch.manual_seed(0)
+    lyr = keras.layers.Dense(1, input_shape=(2,), use_bias=False)
+    m = keras.Sequential([lyr])
+    m.compile(optimizer=keras.optimizers.Adam(lr=0.1), loss="mse")
+    w0 = lyr.weight.detach().clone()
+    x = np.array([[1.0, 2.0]], dtype=np.float32)
+    y = np.array([[0.0]], dtype=np.float32)
+    m.train_on_batch(x, y)
+    pred = float((w0 @ torch.tensor([1.0, 2.0])).item())
+    g = 2 * pred * torch.tensor([1.0, 2.0])
+    mt = 0.1 * g
+    vt = 0.001 * g * g
+    lr_t = 0.1 * math.sqrt(1 - 0.999) / (1 - 0.9)
+    expect = w0[0] - lr_t * mt / (vt.sqrt() + 1e-7)
+    torch.testing.assert_close(lyr.weight.detach()[0], expect, rtol=1e-5, atol=1e-6)

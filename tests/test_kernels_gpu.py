@@ -134,7 +134,7 @@ def test_adam(cuda, adamw, keras_eps):
     if adamw:
         wr = wr * (1 - 1e-3 * 1e-2)
     if keras_eps:
-        den = (vr.sqrt() + 1e-7 * math.sqrt(bc2)) / math.sqrt(bc2)
+        den = (vr.sqrt() + 1e-7) / math.sqrt(bc2)
     else:
         den = vr.sqrt() / math.sqrt(bc2) + 1e-7
     wr = wr - (1e-3 / bc1) * mr / den

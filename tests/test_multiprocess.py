@@ -84,3 +84,8 @@ def test_timeline(tmp_path):
     path = str(tmp_path / "timeline.json")
     run_ranks("timeline", 2, extra_env={"HOROVOD_TIMELINE": path})
     assert os.path.getsize(path) > 0
+
+
+def test_keras_tf2_style_2ranks():
+    outs = run_ranks("keras_tf2", 2, timeout=400)
+    assert "finished gradual learning rate warmup" in outs[0]
