@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Config 5 of BASELINE.json: BERT-Large bf16 pre-training (MLM + NSP, seq 128)
+with fp16 gradient compression + Adasum through mivod.torch.DistributedOptimizer.
+
+    python benchmarks/bench_bert.py --steps 20 --warmup 5
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        benchmarks/bench_bert.py
+Prints one JSON line (sequences/sec for the whole job).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU sequences")
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--model", default="large", choices=["large", "base", "tiny"])
+    ap.add_argument("--compression", default="fp16", choices=["none", "fp16", "bf16"])
+    ap.add_argument("--op", default="adasum", choices=["adasum", "average"])
+    ap.add_argument("--lr", type=float, default=1e-4)
+    args = ap.parse_args()
+
+    import torch
+
+    import mivod.torch as hvd
+    from mivod.models.bert import BertConfig, BertForPreTraining, synthetic_batch
+    from mivod.optim import FusedAdam
+
+    hvd.init()
+    rank, size, dev = hvd.rank(), hvd.size(), hvd.device()
+    cfg = getattr(BertConfig, args.model)()
+    torch.manual_seed(7)
+    model = BertForPreTraining(cfg).to(dev).to(torch.bfloat16)
+    opt = FusedAdam(model.parameters(), lr=args.lr, weight_decay=0.01, adamw=True)
+    op = hvd.Adasum if args.op == "adasum" else hvd.Average
+    opt = hvd.DistributedOptimizer(opt, named_parameters=model.named_parameters(),
+                                   compression=hvd.Compression.by_name(args.compression), op=op)
+    hvd.broadcast_parameters(model.state_dict(), 0)
+    hvd.broadcast_optimizer_state(opt, 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(100 + rank)
+    batch = synthetic_batch(cfg, args.batch, args.seq, dev, generator=g)
+
+    def step():
+        loss = model(*batch)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    t0 = time.perf_counter()
+    for i in range(args.warmup):
+        loss = step()
+        if rank == 0 and i == 0:
+            torch.cuda.synchronize()
+            print(f"[bert] first step {time.perf_counter() - t0:.1f}s", file=sys.stderr,
+                  flush=True)
+    torch.cuda.synchronize()
+    if size > 1:
+        torch.distributed.barrier(device_ids=[dev.index])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if size > 1:
+        torch.distributed.barrier(device_ids=[dev.index])
+    el = time.perf_counter() - t0
+    if size > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({
+            "metric": "sequences/sec (whole node), BERT-Large bf16 pre-training, fp16 compression + Adasum",
+            "value": round(args.batch * size * args.steps / el, 2), "unit": "sequences/sec",
+            "n_gpus": size, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1000, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random token ids, 15% masked positions; random-init weights)",
+            "loss": round(float(loss.detach()), 4),
+            "config": {"model": f"BERT-{args.model}", "global_batch": args.batch * size,
+                       "seq_len": args.seq, "parallelism": f"dp{size}",
+                       "compression": args.compression, "op": args.op,
+                       "optimizer": "mivod FusedAdamW"}}), flush=True)
+    hvd.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -22,6 +22,9 @@ for v in ${VARIANTS:-default}; do
     normal) MIOPEN_FIND_MODE=NORMAL run bench_normal 1200 python bench.py --steps 20 --warmup 10 ;;
     bs512) run bench_bs512 1200 python bench.py --steps 20 --warmup 10 --batch 512 ;;
     bs128) run bench_bs128 1200 python bench.py --steps 20 --warmup 10 --batch 128 ;;
+    bert) run bench_bert 1200 python benchmarks/bench_bert.py --steps 20 --warmup 5 ${BERT_ARGS:-} ;;
+    bertprof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+          run rocprof_bert 1200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bert -o run --output-format csv -- python benchmarks/bench_bert.py --steps 10 --warmup 3 ${BERT_ARGS:-} ;;
     lars) run bench_lars 1200 python bench.py --steps 20 --warmup 10 --optimizer lars ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
           run rocprof 1200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 5 ${BENCH_ARGS:-} ;;
