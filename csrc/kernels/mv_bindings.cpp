@@ -8,6 +8,8 @@
 
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "mv_bn.h"
 #include "mv_kernels.h"
 
@@ -361,6 +363,11 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("lars_step", &lars_step, "fused segmented LARS step");
   m.def("seg_dot3", &seg_dot3, "per-segment (a.b, |a|^2, |b|^2)");
   m.def("adasum_combine", &adasum_combine, "per-segment Adasum merge a <- ca*a + cb*b");
+  // roctx ranges: rocprofv3 --marker-trace shows mivod's bucket phases (pack,
+  // allreduce, fused step) on the same timeline as the kernels and RCCL
+  m.def("range_push", [](const std::string& s) { return roctxRangePushA(s.c_str()); });
+  m.def("range_pop", []() { return roctxRangePop(); });
+  m.def("mark", [](const std::string& s) { roctxMarkA(s.c_str()); });
   m.def("bn_fwd_train", &bn_fwd_train, "fused NHWC BN(+add)(+ReLU) training forward");
   m.def("bn_apply", &bn_apply, "NHWC y = act(x*scale + bias (+res))");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward");

@@ -119,7 +119,8 @@ def build_kernels(verbose: bool = False, force: bool = False) -> str:
     so = kernels_so()
     if force or jobs or _stale(so, objs):
         _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs + ld
-             + ["-L", os.path.join(ROCM, "lib"), "-lamdhip64"], verbose)
+             + ["-L", os.path.join(ROCM, "lib"), f"-Wl,-rpath,{os.path.join(ROCM, 'lib')}",
+                "-lamdhip64", "-lrocprofiler-sdk-roctx"], verbose)
     return so
 
 

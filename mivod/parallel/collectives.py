@@ -53,6 +53,10 @@ def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
     if op == Adasum:
         from .adasum import adasum_allreduce_
         return adasum_allreduce_(t, adasum_table, pg)
+    if (st.config is not None and st.config.hierarchical_allreduce and st.local_pg is not None
+            and st.cross_pg is not None and group is None and not engine
+            and t.is_cuda == (st.backend == "nccl")):
+        return hierarchical_allreduce_(t, op)
     if t.is_cuda:
         rop = dist.ReduceOp.AVG if op == Average else dist.ReduceOp.SUM
         dist.all_reduce(t, op=rop, group=pg)
@@ -70,6 +74,37 @@ def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
     if op == Average:
         w.div_(st.size)
     t.copy_(w)
+    return t
+
+
+def hierarchical_allreduce_(t: torch.Tensor, op: int = Sum) -> torch.Tensor:
+    """HOROVOD_HIERARCHICAL_ALLREDUCE: intra-node reduce-scatter (xGMI), cross-node
+    allreduce of each 1/local_size shard (the network carries 1/L of the bytes),
+    intra-node allgather.  On CPU/gloo (no reduce-scatter) the same two-level
+    structure runs as local allreduce + cross allreduce."""
+    st = basics.state()
+    L = st.local_size
+    flat = t.view(-1) if t.is_contiguous() else t.contiguous().view(-1)
+    if t.is_cuda:
+        n = flat.numel()
+        pad = (-n) % L
+        work = flat if pad == 0 else torch.cat([flat, flat.new_zeros(pad)])
+        shard = torch.empty(work.numel() // L, dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(shard, work, op=dist.ReduceOp.SUM, group=st.local_pg)
+        dist.all_reduce(shard, op=dist.ReduceOp.SUM, group=st.cross_pg)
+        dist.all_gather_into_tensor(work, shard, group=st.local_pg)
+        if pad:
+            flat.copy_(work[:n])
+    else:
+        work = flat if _gloo_ok(flat.dtype) else flat.float()
+        dist.all_reduce(work, op=dist.ReduceOp.SUM, group=st.local_pg)
+        dist.all_reduce(work, op=dist.ReduceOp.SUM, group=st.cross_pg)
+        if work is not flat:
+            flat.copy_(work)
+    if op == Average:
+        flat.div_(st.size)
+    if flat.data_ptr() != t.data_ptr():
+        t.copy_(flat.view_as(t))
     return t
 
 

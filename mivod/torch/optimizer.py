@@ -41,6 +41,7 @@ from ..ops import kernels as K
 from ..ops.compression import Compression
 from ..optim.fused import Arena, FusedOptimizer, _align
 from ..parallel import collectives as C
+from ..utils import markers as MK
 from ..utils import timeline as TL
 
 
@@ -268,8 +269,9 @@ class _DistributedOptimizerMixin:
                 ent = groups.setdefault(g.dtype, ([], []))
                 ent[0].append(g)
                 ent[1].append(lo)
-            for dt, (gl, ol) in groups.items():
-                K.pack(gl, a.grad, ol, scale=prescale)
+            with MK.range(f"mivod.pack.{b.name}"):
+                for dt, (gl, ol) in groups.items():
+                    K.pack(gl, a.grad, ol, scale=prescale)
             if self._mvd_fused:
                 for p in b.params:
                     p.grad = None            # freed on the compute stream after the pack
@@ -285,17 +287,19 @@ class _DistributedOptimizerMixin:
             if cuda:
                 self._mvd_stream.wait_event(ev)
             if size > 1:
-                if self._mvd_op == C.Adasum:
-                    C.allreduce_(flat, C.Adasum, adasum_table=a.table(b.i0, b.i1))
-                elif self._mvd_fused:
-                    C.allreduce_(flat, C.Sum)
-                else:
-                    C.allreduce_(flat, C.Average if self._mvd_op == C.Average else C.Sum)
+                with MK.range(f"mivod.allreduce.{b.name}"):
+                    if self._mvd_op == C.Adasum:
+                        C.allreduce_(flat, C.Adasum, adasum_table=a.table(b.i0, b.i1))
+                    elif self._mvd_fused:
+                        C.allreduce_(flat, C.Sum)
+                    else:
+                        C.allreduce_(flat, C.Average if self._mvd_op == C.Average else C.Sum)
             if self._mvd_fused:
                 gscale = 1.0
                 if self._mvd_op == C.Average:
                     gscale = self._mvd_predivide / size
-                self._mv_apply(a, b.i0, b.i1, gscale)
+                with MK.range(f"mivod.step.{b.name}"):
+                    self._mv_apply(a, b.i0, b.i1, gscale)
             else:
                 post = self._mvd_predivide if (self._mvd_op == C.Average and size > 1) else 1.0
                 if post != 1.0:

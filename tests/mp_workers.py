@@ -318,6 +318,24 @@ def keras_tf2():
     print("OK", r)
 
 
+def hierarchical():
+    """2 'nodes' x 2 local ranks: HOROVOD_HIERARCHICAL_ALLREDUCE gives the same
+    result as the flat allreduce; local/cross topology exposed."""
+    os.environ["HOROVOD_HIERARCHICAL_ALLREDUCE"] = "1"
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    assert hvd.local_size() == 2 and hvd.cross_size() == 2
+    assert hvd.local_rank() == r % 2 and hvd.cross_rank() == r // 2
+    from mivod.common import basics
+    assert basics.state().local_pg is not None and basics.state().cross_pg is not None
+    x = torch.arange(7, dtype=torch.float32) + r
+    _close(hvd.allreduce(x, op=hvd.Sum, name="h1"), torch.arange(7, dtype=torch.float32) * n +
+           sum(range(n)))
+    _close(hvd.allreduce(x, name="h2"), torch.arange(7, dtype=torch.float32) + (n - 1) / 2)
+    hvd.shutdown()
+    print("OK", r)
+
+
 def hvd_rank():
     return int(os.environ.get("RANK", "0"))
 

@@ -19,13 +19,14 @@ def free_port():
     return p
 
 
-def run_ranks(scenario, n=2, timeout=240, extra_env=None):
+def run_ranks(scenario, n=2, timeout=240, extra_env=None, local_size=None):
     port = free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ)
+        ls = local_size or n
         env.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(r),
-                    "WORLD_SIZE": str(n), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(n),
+                    "WORLD_SIZE": str(n), "LOCAL_RANK": str(r % ls), "LOCAL_WORLD_SIZE": str(ls),
                     "MIVOD_TRANSPORT": "gloo", "OMP_NUM_THREADS": "1",
                     "PYTHONPATH": ROOT + os.pathsep + env.get("PYTHONPATH", "")})
         env.pop("HOROVOD_RANK", None)
@@ -89,3 +90,7 @@ def test_timeline(tmp_path):
 def test_keras_tf2_style_2ranks():
     outs = run_ranks("keras_tf2", 2, timeout=400)
     assert "finished gradual learning rate warmup" in outs[0]
+
+
+def test_hierarchical_allreduce_2x2():
+    run_ranks("hierarchical", 4, local_size=2)
