@@ -150,6 +150,7 @@ class _DistributedOptimizerMixin:
             raise ValueError(basics._NOT_INIT)
         cfg = st.config
         self._mvd_size = st.size
+        self._mvd_rank = st.rank
         self._mvd_compression = compression
         self._mvd_bpps = int(backward_passes_per_step)
         self._mvd_op = op
@@ -215,6 +216,13 @@ class _DistributedOptimizerMixin:
         self._mvd_stream = st.comm_stream
         self._mvd_done_event = None
         self._mvd_nonfinite = None
+        self._mvd_steps = 0
+        self._mvd_autotune = None
+        if cfg.autotune and bucket_mb is None and first_bucket_mb is None:
+            from ..parallel.autotune import BucketAutotuner
+            self._mvd_autotune = BucketAutotuner(log_path=cfg.autotune_log)
+            f0, b0 = self._mvd_autotune.current()
+            self._mvd_replan(f0, b0)
         self._mvd_hooks = []
         for p in trainable:
             self._mvd_hooks.append(p.register_post_accumulate_grad_hook(self._mvd_hook))
@@ -259,6 +267,8 @@ class _DistributedOptimizerMixin:
                 if g is None:
                     a.grad[lo:lo + p.numel()].zero_()
                     continue
+                if g.is_sparse:
+                    g = g.to_dense()          # sparse_as_dense (embedding grads)
                 if g.data_ptr() == a.grad.data_ptr() + lo * a.grad.element_size() and \
                         g.dtype == a.grad.dtype and g.stride() == p.stride():
                     if prescale != 1.0:
@@ -350,6 +360,31 @@ class _DistributedOptimizerMixin:
             self._mvd_next = 0
             self._mvd_in_step = False
             self._mvd_synchronized = True
+            self._mvd_steps += 1
+            if self._mvd_autotune is not None and not self._mvd_autotune.done:
+                self._mvd_autotune_step()
+        from ..utils import faults
+        faults.maybe_inject(self._mvd_rank, self._mvd_steps)
+
+    def _mvd_replan(self, first_mb: float, bucket_mb: float):
+        self._mvd_buckets = plan_buckets(self._mvd_arenas, int(first_mb * 2 ** 20),
+                                         int(bucket_mb * 2 ** 20), self._mvd_position)
+        self._mvd_where = {}
+        for b in self._mvd_buckets:
+            for k, p in enumerate(b.params):
+                self._mvd_where[id(p)] = (b, b.i0 + k)
+
+    def _mvd_autotune_step(self):
+        def sync():
+            if self._mvd_stream is not None:
+                torch.cuda.synchronize()
+        cand = self._mvd_autotune.on_step_end(sync)
+        if cand is None:
+            return
+        if self._mvd_size > 1:           # everybody adopts rank 0's decision
+            from .functions import broadcast_object
+            cand = broadcast_object(cand, root_rank=0)
+        self._mvd_replan(*cand)
 
     @contextlib.contextmanager
     def skip_synchronize(self):
