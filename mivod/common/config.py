@@ -14,6 +14,8 @@ mivod extensions (MI355X-specific):
                              one xGMI link finishes a bucket in well under 1 ms)
   ``MIVOD_FIRST_BUCKET_MB``  first (= last layers') bucket, small to start xGMI
                              traffic early (default 2 MB)
+  ``MIVOD_LAST_BUCKET_MB``   last (= first layers') bucket, small so the exposed
+                             allreduce + step after backward ends is short (4 MB)
   ``MIVOD_TRANSPORT``        ``rccl`` (default on GPU) | ``gloo`` (CPU)
   ``MIVOD_COMPRESSION``      default wire compression for DistributedOptimizer
   ``MIVOD_COMM_PRIORITY``    ``high`` (default) | ``normal`` HIP stream priority
@@ -62,6 +64,7 @@ class Config:
     hierarchical_allreduce: bool = False
     bucket_mb: float = 32.0
     first_bucket_mb: float = 2.0
+    last_bucket_mb: float = 4.0
     transport: str = ""
     compression: str = "none"
     comm_priority: str = "high"
@@ -86,6 +89,7 @@ class Config:
         c.hierarchical_allreduce = _env_bool("HOROVOD_HIERARCHICAL_ALLREDUCE")
         c.bucket_mb = _env_float("MIVOD_BUCKET_MB", c.bucket_mb)
         c.first_bucket_mb = _env_float("MIVOD_FIRST_BUCKET_MB", c.first_bucket_mb)
+        c.last_bucket_mb = _env_float("MIVOD_LAST_BUCKET_MB", c.last_bucket_mb)
         c.transport = os.environ.get("MIVOD_TRANSPORT", "").lower()
         c.compression = os.environ.get("MIVOD_COMPRESSION", "none").lower()
         c.comm_priority = os.environ.get("MIVOD_COMM_PRIORITY", "high").lower()

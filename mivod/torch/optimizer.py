@@ -101,12 +101,17 @@ class _Bucket:
         return (self.hi - self.lo) * self.arena.grad.element_size()
 
 
-def plan_buckets(arenas, first_bucket_bytes: int, bucket_bytes: int, position) -> List[_Bucket]:
+def plan_buckets(arenas, first_bucket_bytes: int, bucket_bytes: int, position,
+                 last_bucket_bytes: int = 0) -> List[_Bucket]:
     """Split every arena (params in backward order) into contiguous buckets.
 
     The first bucket of the whole model (earliest in backward) is capped at
-    ``first_bucket_bytes``; the rest at ``bucket_bytes``.  Buckets are ordered
-    by the backward position of their first parameter, identically on all ranks.
+    ``first_bucket_bytes`` so xGMI traffic starts early; the last one (the
+    first layers, whose gradients arrive when backward is already over) at
+    ``last_bucket_bytes`` so the exposed tail — its allreduce + fused step after
+    the final backward kernel — stays short; the rest at ``bucket_bytes``.
+    Buckets are ordered by readiness (backward position of their last
+    parameter), identically on all ranks.
     """
     raw = []
     for a in arenas:
@@ -115,28 +120,40 @@ def plan_buckets(arenas, first_bucket_bytes: int, bucket_bytes: int, position) -
         cur = 0
         for i, p in enumerate(a.params):
             sz = _align(p.numel()) * es
-            cap = bucket_bytes
-            if cur > 0 and cur + sz > cap:
+            if cur > 0 and cur + sz > bucket_bytes:
                 raw.append((a, i0, i))
                 i0, cur = i, 0
             cur += sz
         raw.append((a, i0, len(a.params)))
-    # split the globally-first bucket down to first_bucket_bytes
-    raw.sort(key=lambda r: min(position[id(p)] for p in r[0].params[r[1]:r[2]]))
-    if raw and first_bucket_bytes > 0:
-        a, i0, i1 = raw[0]
+
+    def key(r):
+        # a bucket is ready when its LAST gradient arrives: order (and launch)
+        # buckets by that, or a bucket holding one early-layer tensor (e.g. the
+        # stem BatchNorm in the fp32 arena) would block every later launch
+        return max(position[id(p)] for p in r[0].params[r[1]:r[2]])
+
+    def split(r, cap, from_end):
+        a, i0, i1 = r
         es = a.grad.element_size()
-        cur, cut = 0, i1
-        for i in range(i0, i1):
+        rng = range(i1 - 1, i0 - 1, -1) if from_end else range(i0, i1)
+        cur = 0
+        for i in rng:
             cur += _align(a.params[i].numel()) * es
-            if cur >= first_bucket_bytes:
-                cut = i + 1
-                break
-        if cut < i1:
-            raw[0:1] = [(a, i0, cut), (a, cut, i1)]
-    raw.sort(key=lambda r: min(position[id(p)] for p in r[0].params[r[1]:r[2]]))
-    return [_Bucket(k, a, i0, i1, min(position[id(p)] for p in a.params[i0:i1]))
-            for k, (a, i0, i1) in enumerate(raw)]
+            if cur >= cap:
+                cut = i if from_end else i + 1
+                if i0 < cut < i1:
+                    return [(a, i0, cut), (a, cut, i1)]
+                return [r]
+        return [r]
+
+    raw.sort(key=key)
+    if raw and first_bucket_bytes > 0:
+        raw[0:1] = split(raw[0], first_bucket_bytes, False)
+    raw.sort(key=key)
+    if len(raw) > 1 and last_bucket_bytes > 0:
+        raw[-1:] = split(raw[-1], last_bucket_bytes, True)
+    raw.sort(key=key)
+    return [_Bucket(k, a, i0, i1, key((a, i0, i1))) for k, (a, i0, i1) in enumerate(raw)]
 
 
 class _DistributedOptimizerMixin:
@@ -202,8 +219,9 @@ class _DistributedOptimizerMixin:
         self._mvd_arenas = arenas
         bmb = cfg.bucket_mb if bucket_mb is None else bucket_mb
         fmb = cfg.first_bucket_mb if first_bucket_mb is None else first_bucket_mb
+        self._mvd_last_bytes = int(cfg.last_bucket_mb * 2 ** 20)
         self._mvd_buckets = plan_buckets(arenas, int(fmb * 2 ** 20), int(bmb * 2 ** 20),
-                                         self._mvd_position)
+                                         self._mvd_position, self._mvd_last_bytes)
         self._mvd_where: Dict[int, tuple] = {}
         for b in self._mvd_buckets:
             for k, p in enumerate(b.params):
@@ -368,7 +386,8 @@ class _DistributedOptimizerMixin:
 
     def _mvd_replan(self, first_mb: float, bucket_mb: float):
         self._mvd_buckets = plan_buckets(self._mvd_arenas, int(first_mb * 2 ** 20),
-                                         int(bucket_mb * 2 ** 20), self._mvd_position)
+                                         int(bucket_mb * 2 ** 20), self._mvd_position,
+                                         self._mvd_last_bytes)
         self._mvd_where = {}
         for b in self._mvd_buckets:
             for k, p in enumerate(b.params):

@@ -80,3 +80,24 @@ def test_launch_failure_kills_all(tmp_path):
                        timeout=60)
     assert r.returncode == 3, r.stdout + r.stderr
     assert "rank 1 exited with code 3" in r.stderr
+
+
+def test_bucket_plan_orders_by_readiness():
+    """Buckets launch in the order their last gradient arrives; the mixed
+    bf16-conv / fp32-BN ResNet-50 layout must not let the BN bucket (which
+    holds the stem BN) block the conv buckets."""
+    import mivod.torch as hvd
+    from mivod.models.resnet import resnet50, to_mixed_bf16
+    from mivod.optim import FusedSGD
+    hvd.init()
+    m = to_mixed_bf16(resnet50())
+    opt = hvd.DistributedOptimizer(FusedSGD(m.parameters(), lr=0.1, momentum=0.9),
+                                   named_parameters=m.named_parameters())
+    names = [n for n, _ in m.named_parameters()]
+    pos = {n: len(names) - 1 - i for i, n in enumerate(names)}      # backward position
+    plan = opt.bucket_plan()
+    ready = [max(pos[p] for p in ps) for _, _, ps in plan]
+    assert ready == sorted(ready)
+    assert plan[0][1] <= 4 * 2 ** 20            # small first bucket
+    assert plan[-1][1] <= 5 * 2 ** 20           # small exposed tail
+    assert sum(b for _, b, _ in plan) >= 25557032 * 2 * 0.99
