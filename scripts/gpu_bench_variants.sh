@@ -21,6 +21,8 @@ for v in ${VARIANTS:-default}; do
     default) run bench_default 1200 python bench.py --steps 20 --warmup 10 ;;
     normal) MIOPEN_FIND_MODE=NORMAL run bench_normal 1200 python bench.py --steps 20 --warmup 10 ;;
     bs512) run bench_bs512 1200 python bench.py --steps 20 --warmup 10 --batch 512 ;;
+    bs768) run bench_bs768 1500 python bench.py --steps 15 --warmup 8 --batch 768 ;;
+    bs1024) run bench_bs1024 1500 python bench.py --steps 15 --warmup 8 --batch 1024 ;;
     bs128) run bench_bs128 1200 python bench.py --steps 20 --warmup 10 --batch 128 ;;
     bert) run bench_bert 1200 python benchmarks/bench_bert.py --steps 20 --warmup 5 ${BERT_ARGS:-} ;;
     bertprof) cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
