@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("MIVOD_BENCH_BATCH", 256)),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("MIVOD_BENCH_BATCH", 512)),
                     help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lars", "torch-sgd"])
