@@ -10,6 +10,7 @@
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include "mv_attn.h"
 #include "mv_bn.h"
 #include "mv_kernels.h"
 
@@ -349,6 +350,75 @@ std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
   return {dx, dg, db, dz};
 }
 
+// ---------------------------------------------------------------------------
+// Fused MFMA attention (head dim 64)
+// ---------------------------------------------------------------------------
+AttnParams attn_params(const at::Tensor& qkv, const c10::optional<at::Tensor>& mask,
+                       double p_drop, int64_t seed) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.is_contiguous(),
+              "attn: qkv must be a contiguous bf16 GPU tensor");
+  TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == 64,
+              "attn: qkv must be [b, s, 3, h, 64]");
+  AttnParams p{};
+  p.qkv = qkv.data_ptr();
+  p.b = (int)qkv.size(0);
+  p.s = (int)qkv.size(1);
+  p.h = (int)qkv.size(3);
+  p.scale_log2 = (float)(1.4426950408889634 / 8.0);
+  p.mask = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kFloat && mask->is_contiguous() &&
+                mask->numel() == (int64_t)p.b * p.s, "attn: mask must be fp32 [b, s]");
+    p.mask = mask->data_ptr<float>();
+  }
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "attn: dropout must be in [0, 1)");
+  p.p_drop = (float)p_drop;
+  p.seed = (uint32_t)seed;
+  p.thresh = (uint32_t)std::min(4294967295.0, p_drop * 4294967296.0);
+  return p;
+}
+
+std::vector<at::Tensor> attn_fwd(at::Tensor qkv, c10::optional<at::Tensor> mask, double p_drop,
+                                 int64_t seed) {
+  c10::DeviceGuard guard(qkv.device());
+  AttnParams p = attn_params(qkv, mask, p_drop, seed);
+  at::Tensor out = at::empty({p.b, p.s, p.h, 64}, qkv.options());
+  at::Tensor lse = at::empty({p.b, p.h, p.s}, qkv.options().dtype(at::kFloat));
+  p.out = out.data_ptr();
+  p.lse = lse.data_ptr<float>();
+  mv_attn_fwd(p, cur_stream());
+  return {out, lse};
+}
+
+at::Tensor attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse,
+                    c10::optional<at::Tensor> mask, double p_drop, int64_t seed) {
+  c10::DeviceGuard guard(qkv.device());
+  AttnParams p = attn_params(qkv, mask, p_drop, seed);
+  TORCH_CHECK(out.is_contiguous() && dout.is_contiguous() && out.sizes() == dout.sizes() &&
+              out.numel() == (int64_t)p.b * p.s * p.h * 64 &&
+              dout.scalar_type() == at::kBFloat16, "attn_bwd: out/dout must be bf16 [b,s,h,64]");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)p.b * p.h * p.s, "attn_bwd: lse");
+  p.lse = lse.data_ptr<float>();
+  auto fo = qkv.options().dtype(at::kFloat);
+  const int nkb = (p.s + 63) / 64;
+  at::Tensor delta = at::empty({p.b, p.h, p.s}, fo);
+  at::Tensor dq_part = at::empty({(int64_t)nkb * p.b * p.s * p.h * 64}, fo);
+  at::Tensor dqkv = at::empty_like(qkv);
+  mv_attn_bwd(p, out.data_ptr(), dout.data_ptr(), delta.data_ptr<float>(),
+              dq_part.data_ptr<float>(), dqkv.data_ptr(), cur_stream());
+  return dqkv;
+}
+
+at::Tensor attn_dropout_mask(int64_t b, int64_t h, int64_t s, double p_drop, int64_t seed,
+                             at::Device device) {
+  c10::DeviceGuard guard(device);
+  at::Tensor keep = at::empty({b, h, s, s}, at::TensorOptions().dtype(at::kByte).device(device));
+  const uint32_t th = (uint32_t)std::min(4294967295.0, p_drop * 4294967296.0);
+  mv_attn_dropout_mask((int)b, (int)h, (int)s, (uint32_t)seed, th, keep.data_ptr<uint8_t>(),
+                       cur_stream());
+  return keep;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -368,6 +438,9 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("range_push", [](const std::string& s) { return roctxRangePushA(s.c_str()); });
   m.def("range_pop", []() { return roctxRangePop(); });
   m.def("mark", [](const std::string& s) { roctxMarkA(s.c_str()); });
+  m.def("attn_fwd", &attn_fwd, "fused MFMA attention forward -> (out [b,s,h,64], lse)");
+  m.def("attn_bwd", &attn_bwd, "fused MFMA attention backward -> dqkv");
+  m.def("attn_dropout_mask", &attn_dropout_mask, "dropout keep-mask of the fused attention");
   m.def("bn_fwd_train", &bn_fwd_train, "fused NHWC BN(+add)(+ReLU) training forward");
   m.def("bn_apply", &bn_apply, "NHWC y = act(x*scale + bias (+res))");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward");
