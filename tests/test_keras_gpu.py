@@ -1,0 +1,26 @@
+"""Keras front end on the GPU: the TF2-style example (config 2) and the ConvNet
+(config 1) train on cuda:0 through mivod's fused optimizers."""
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "examples"))
+
+
+def test_tf2_style_example_on_gpu(cuda, tmp_path, monkeypatch):
+    monkeypatch.setenv("PS_MODEL_PATH", str(tmp_path))
+    from keras_mnist_tf2_style import main
+    hist, model = main(["--epochs", "2", "--steps", "40"])
+    assert next(model.parameters()).is_cuda
+    assert hist.history["loss"][-1] < hist.history["loss"][0]
+
+
+def test_convnet_example_on_gpu(cuda, tmp_path, monkeypatch):
+    monkeypatch.setenv("PS_MODEL_PATH", str(tmp_path))
+    from keras_mnist_convnet import main
+    hist, score = main(["--epochs", "1", "--train-samples", "12800", "--no-export"])
+    assert score[1] > 0.9, score
