@@ -1,0 +1,381 @@
+// Fused transformer elementwise kernels (BERT) for gfx950.
+//
+//  * bias_gelu       y = gelu(x + b)             (x = GEMM output without bias)
+//    backward        dx = dy * gelu'(x + b), dbias = sum_rows dx  (one pass)
+//  * bias_dropout_add_ln
+//                    v = res + dropout(z + b);  y = LN(v) * gamma + beta
+//    backward        dv = LN'(dy) (the residual's grad), dz = dropout'(dv),
+//                    dgamma / dbeta / dbias column sums            (one pass)
+//
+// Replaces, per BERT layer, torch's separate bias-add (inside the GEMM), GELU,
+// dropout, residual add, LayerNorm and their backward kernels plus the
+// bias-gradient reductions (profiles/r1_bert_large_fused_attention.md).
+// Dropout masks come from a counter hash of (seed, row, col) — no mask tensor.
+//
+// Row kernels: one wave per row (wave64, 8 bf16 per lane per 512-column chunk,
+// all chunks held in registers, H <= 4096, H % 512 == 0 or H % 8 == 0 with
+// guards); row statistics by wave shuffles.  Column sums: each lane owns fixed
+// columns across the rows its wave processes, waves combine through LDS in a
+// fixed order, one partial row per workgroup, then a fixed-order finalize
+// kernel — deterministic.
+#include "mv_bert.h"
+#include "mv_common.h"
+
+namespace mv {
+namespace tx {
+
+constexpr int kRowsPerBlock = 32;      // 4 waves x 8 rows
+constexpr float kSqrt1_2 = 0.70710678118654752f;
+constexpr float kInvSqrt2Pi = 0.39894228040143268f;
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ bool keep(uint32_t seed, uint32_t row, uint32_t col, uint32_t th) {
+  return mix32(mix32(seed + row * 0x9E3779B1u) + col * 0x85EBCA6Bu) >= th;
+}
+
+__device__ __forceinline__ float gelu(float v) { return 0.5f * v * (1.f + erff(v * kSqrt1_2)); }
+__device__ __forceinline__ float gelu_grad(float v) {
+  return 0.5f * (1.f + erff(v * kSqrt1_2)) + v * kInvSqrt2Pi * __expf(-0.5f * v * v);
+}
+
+// --------------------------------------------------------------- bias + GELU
+// 2-D geometry: a workgroup owns columns [c0, c0 + 2048) (256 lanes x 8) and
+// a range of rows; each lane keeps its 8 columns' bias and partial sums.
+__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const __bf16* __restrict__ x,
+                                                             const __bf16* __restrict__ b,
+                                                             __bf16* __restrict__ y, int64_t M,
+                                                             int N, int64_t rows_per_block) {
+  const int c = blockIdx.y * 2048 + threadIdx.x * 8;
+  if (c >= N) return;
+  float bv[8];
+  load8(b + c, bv);
+  const int64_t r0 = blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[8];
+    load8(x + r * N + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu(v[j] + bv[j]);
+    store8(y + r * N + c, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const __bf16* __restrict__ dy,
+                                                             const __bf16* __restrict__ x,
+                                                             const __bf16* __restrict__ b,
+                                                             __bf16* __restrict__ dx,
+                                                             float* __restrict__ partial,
+                                                             int64_t M, int N,
+                                                             int64_t rows_per_block) {
+  const int c = blockIdx.y * 2048 + threadIdx.x * 8;
+  if (c >= N) return;
+  float bv[8], acc[8];
+  load8(b + c, bv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const int64_t r0 = blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[8], g[8];
+    load8(x + r * N + c, v);
+    load8(dy + r * N + c, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] *= gelu_grad(v[j] + bv[j]);
+      acc[j] += g[j];
+    }
+    store8(dx + r * N + c, g);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) partial[(int64_t)blockIdx.x * N + c + j] = acc[j];
+}
+
+// column sums of [P][N] partials (fixed order) -> bf16 / fp32 output
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ partial, int P,
+                                                      int N, __bf16* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int p = 0;
+  for (; p + 3 < P; p += 4) {
+    s0 += partial[(int64_t)p * N + c];
+    s1 += partial[(int64_t)(p + 1) * N + c];
+    s2 += partial[(int64_t)(p + 2) * N + c];
+    s3 += partial[(int64_t)(p + 3) * N + c];
+  }
+  for (; p < P; ++p) s0 += partial[(int64_t)p * N + c];
+  out[c] = (__bf16)((s0 + s1) + (s2 + s3));
+}
+
+__global__ __launch_bounds__(256) void colsum_strided_kernel(const float* __restrict__ partial,
+                                                              int P, int N, int64_t stride,
+                                                              __bf16* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  float s0 = 0.f, s1 = 0.f;
+  int p = 0;
+  for (; p + 1 < P; p += 2) {
+    s0 += partial[(int64_t)p * stride + c];
+    s1 += partial[(int64_t)(p + 1) * stride + c];
+  }
+  if (p < P) s0 += partial[(int64_t)p * stride + c];
+  out[c] = (__bf16)(s0 + s1);
+}
+
+// ------------------------------------------------- bias + dropout + add + LN
+struct LnArgs {
+  const __bf16* z;      // [M, H] GEMM output (no bias)
+  const __bf16* bias;   // [H] or null
+  const __bf16* res;    // [M, H] residual or null
+  const __bf16* gamma;  // [H]
+  const __bf16* beta;   // [H]
+  __bf16* v;            // [M, H] saved pre-LN sum
+  __bf16* y;            // [M, H]
+  float* mean;          // [M]
+  float* rstd;          // [M]
+  int64_t M;
+  int H;
+  float eps;
+  float p_drop;
+  uint32_t seed;
+  uint32_t thresh;
+};
+
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.M) return;
+  const float inv_keep = a.p_drop > 0.f ? 1.f / (1.f - a.p_drop) : 1.f;
+  float v[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = k * 512 + lane * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
+    if (c < a.H) {
+      float z[8], bb[8], rr[8];
+      load8(a.z + row * a.H + c, z);
+      if (a.bias) load8(a.bias + c, bb);
+      if (a.res) load8(a.res + row * a.H + c, rr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = z[j] + (a.bias ? bb[j] : 0.f);
+        if (a.p_drop > 0.f)
+          t = keep(a.seed, (uint32_t)row, (uint32_t)(c + j), a.thresh) ? t * inv_keep : 0.f;
+        t += a.res ? rr[j] : 0.f;
+        v[k][j] = (float)(__bf16)t;     // stats on the stored (bf16) value
+        s += v[k][j];
+      }
+      if (a.v) store8(a.v + row * a.H + c, v[k]);
+    }
+  }
+  const float mean = wave_sum(s) / (float)a.H;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    if (k * 512 + lane * 8 < a.H) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[k][j] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)a.H + a.eps);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = k * 512 + lane * 8;
+    if (c < a.H) {
+      float gm[8], bt[8], o[8];
+      load8(a.gamma + c, gm);
+      load8(a.beta + c, bt);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * gm[j] + bt[j];
+      store8(a.y + row * a.H + c, o);
+    }
+  }
+  if (lane == 0) {
+    a.mean[row] = mean;
+    a.rstd[row] = rstd;
+  }
+}
+
+struct LnBwdArgs {
+  const __bf16* dy;     // [M, H]
+  const __bf16* v;      // [M, H] saved pre-LN sum
+  const float* mean;    // [M]
+  const float* rstd;    // [M]
+  const __bf16* gamma;  // [H]
+  __bf16* dv;           // [M, H] grad of the sum (= residual grad)
+  __bf16* dz;           // [M, H] grad of z (dropout backward), or null
+  float* partial;       // [P][3][H]: dgamma, dbeta, dbias(= sum dz)
+  int64_t M;
+  int H;
+  float p_drop;
+  uint32_t seed;
+  uint32_t thresh;
+};
+
+// Write one wave-partial set (this wave's 8 x NCH columns) into LDS slot w, then
+// combine the 4 waves in fixed order into partial row `which` of this block.
+template <int NCH>
+__device__ __forceinline__ void block_colsum(const float (&src)[NCH][8], float (*red)[512],
+                                             float* __restrict__ dst, int H) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = src[k][j];
+    __syncthreads();
+    for (int t = threadIdx.x; t < 512; t += 256) {
+      const int c = k * 512 + t;
+      if (c < H) dst[c] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    }
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float inv_keep = a.p_drop > 0.f ? 1.f / (1.f - a.p_drop) : 1.f;
+  float dg[NCH][8], db[NCH][8], dzs[NCH][8];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dg[k][j] = db[k][j] = dzs[k][j] = 0.f;
+  const int64_t rbeg = (int64_t)blockIdx.x * kRowsPerBlock + w * (kRowsPerBlock / 4);
+  for (int rr = 0; rr < kRowsPerBlock / 4; ++rr) {
+    const int64_t row = rbeg + rr;
+    if (row >= a.M) break;
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float xh[NCH][8], g[NCH][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = k * 512 + lane * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xh[k][j] = g[k][j] = 0.f;
+      if (c < a.H) {
+        float dy[8], vv[8], gm[8];
+        load8(a.dy + row * a.H + c, dy);
+        load8(a.v + row * a.H + c, vv);
+        load8(a.gamma + c, gm);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[k][j] = (vv[j] - mean) * rstd;
+          g[k][j] = dy[j] * gm[j];
+          s1 += g[k][j];
+          s2 += g[k][j] * xh[k][j];
+          dg[k][j] += dy[j] * xh[k][j];
+          db[k][j] += dy[j];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / (float)a.H;
+    s2 = wave_sum(s2) / (float)a.H;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = k * 512 + lane * 8;
+      if (c < a.H) {
+        float d[8], z[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          d[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2);
+          float t = d[j];
+          if (a.p_drop > 0.f)
+            t = keep(a.seed, (uint32_t)row, (uint32_t)(c + j), a.thresh) ? t * inv_keep : 0.f;
+          z[j] = t;
+          dzs[k][j] += t;
+        }
+        store8(a.dv + row * a.H + c, d);
+        if (a.dz) store8(a.dz + row * a.H + c, z);
+      }
+    }
+  }
+  __shared__ float red[4][512];
+  float* base = a.partial + (int64_t)blockIdx.x * 3 * a.H;
+  block_colsum<NCH>(dg, red, base, a.H);
+  block_colsum<NCH>(db, red, base + a.H, a.H);
+  block_colsum<NCH>(dzs, red, base + 2 * a.H, a.H);
+}
+
+}  // namespace tx
+}  // namespace mv
+
+using namespace mv::tx;
+
+static int64_t rows_per_block_for(int64_t M, int N, int64_t* P) {
+  const int gy = (N + 2047) / 2048;
+  int64_t blocks = 1024 / gy;
+  if (blocks < 1) blocks = 1;
+  int64_t rpb = (M + blocks - 1) / blocks;
+  if (rpb < 8) rpb = 8;
+  *P = (M + rpb - 1) / rpb;
+  return rpb;
+}
+
+int64_t mv_bias_gelu_partials(int64_t M, int N) {
+  int64_t P;
+  rows_per_block_for(M, N, &P);
+  return P;
+}
+
+void mv_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t M, int N, hipStream_t st) {
+  int64_t P;
+  const int64_t rpb = rows_per_block_for(M, N, &P);
+  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3((unsigned)P, (N + 2047) / 2048), dim3(256), 0, st,
+                     (const __bf16*)x, (const __bf16*)b, (__bf16*)y, M, N, rpb);
+}
+
+void mv_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, float* partial,
+                      void* dbias, int64_t M, int N, hipStream_t st) {
+  int64_t P;
+  const int64_t rpb = rows_per_block_for(M, N, &P);
+  hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3((unsigned)P, (N + 2047) / 2048), dim3(256), 0, st,
+                     (const __bf16*)dy, (const __bf16*)x, (const __bf16*)b, (__bf16*)dx, partial,
+                     M, N, rpb);
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256), dim3(256), 0, st,
+                     (const float*)partial, (int)P, N, (__bf16*)dbias);
+}
+
+int64_t mv_ln_partials(int64_t M) { return (M + kRowsPerBlock - 1) / kRowsPerBlock; }
+
+void mv_ln_fwd(const LnFwdParams& p, hipStream_t st) {
+  LnArgs a{(const __bf16*)p.z, (const __bf16*)p.bias, (const __bf16*)p.res,
+           (const __bf16*)p.gamma, (const __bf16*)p.beta, (__bf16*)p.v, (__bf16*)p.y, p.mean,
+           p.rstd, p.M, p.H, p.eps, p.p_drop, p.seed, p.thresh};
+  const dim3 g((unsigned)((p.M + 3) / 4));
+  if (p.H <= 512) hipLaunchKernelGGL(ln_fwd_kernel<1>, g, dim3(256), 0, st, a);
+  else if (p.H <= 1024) hipLaunchKernelGGL(ln_fwd_kernel<2>, g, dim3(256), 0, st, a);
+  else if (p.H <= 2048) hipLaunchKernelGGL(ln_fwd_kernel<4>, g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ln_fwd_kernel<8>, g, dim3(256), 0, st, a);
+}
+
+void mv_ln_bwd(const LnBwdParams& p, void* dgamma, void* dbeta, void* dbias, hipStream_t st) {
+  LnBwdArgs a{(const __bf16*)p.dy, (const __bf16*)p.v, p.mean, p.rstd, (const __bf16*)p.gamma,
+              (__bf16*)p.dv, (__bf16*)p.dz, p.partial, p.M, p.H, p.p_drop, p.seed, p.thresh};
+  const int64_t P = mv_ln_partials(p.M);
+  const dim3 g((unsigned)P);
+  if (p.H <= 512) hipLaunchKernelGGL(ln_bwd_kernel<1>, g, dim3(256), 0, st, a);
+  else if (p.H <= 1024) hipLaunchKernelGGL(ln_bwd_kernel<2>, g, dim3(256), 0, st, a);
+  else if (p.H <= 2048) hipLaunchKernelGGL(ln_bwd_kernel<4>, g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ln_bwd_kernel<8>, g, dim3(256), 0, st, a);
+  // partial layout [P][3][H]: column sums with row stride 3H, one launch each
+  void* outs[3] = {dgamma, dbeta, dbias};
+  for (int w = 0; w < 3; ++w) {
+    if (!outs[w]) continue;
+    hipLaunchKernelGGL(colsum_strided_kernel, dim3((p.H + 255) / 256), dim3(256), 0, st,
+                       (const float*)p.partial + (int64_t)w * p.H, (int)P, p.H, 3 * p.H,
+                       (__bf16*)outs[w]);
+  }
+}

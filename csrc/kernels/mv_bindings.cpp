@@ -11,6 +11,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "mv_attn.h"
+#include "mv_bert.h"
 #include "mv_bn.h"
 #include "mv_kernels.h"
 
@@ -419,6 +420,129 @@ at::Tensor attn_dropout_mask(int64_t b, int64_t h, int64_t s, double p_drop, int
   return keep;
 }
 
+// ---------------------------------------------------------------------------
+// Fused transformer elementwise ops (bias+GELU, bias+dropout+residual+LayerNorm)
+// ---------------------------------------------------------------------------
+void check_rows(const at::Tensor& t, int64_t M, int64_t N, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous(),
+              "tx: ", what, " must be a contiguous bf16 GPU tensor");
+  TORCH_CHECK(t.numel() == M * N, "tx: ", what, " has ", t.numel(), " elements, expected ",
+              M * N);
+}
+uint32_t drop_thresh(double p) {
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "tx: dropout must be in [0, 1)");
+  return (uint32_t)std::min(4294967295.0, p * 4294967296.0);
+}
+
+at::Tensor bias_gelu_fwd(at::Tensor x, at::Tensor b) {
+  c10::DeviceGuard guard(x.device());
+  const int64_t N = b.numel(), M = N ? x.numel() / N : 0;
+  TORCH_CHECK(N % 8 == 0 && x.size(-1) == N, "bias_gelu: last dim must equal bias size (%8)");
+  check_rows(x, M, N, "x");
+  check_rows(b, 1, N, "bias");
+  at::Tensor y = at::empty_like(x);
+  if (M) mv_bias_gelu_fwd(x.data_ptr(), b.data_ptr(), y.data_ptr(), M, (int)N, cur_stream());
+  return y;
+}
+
+std::vector<at::Tensor> bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor b) {
+  c10::DeviceGuard guard(x.device());
+  const int64_t N = b.numel(), M = N ? x.numel() / N : 0;
+  TORCH_CHECK(N % 8 == 0 && x.size(-1) == N, "bias_gelu: last dim must equal bias size (%8)");
+  check_rows(x, M, N, "x");
+  check_rows(dy, M, N, "dy");
+  check_rows(b, 1, N, "bias");
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor db = at::zeros_like(b);
+  if (M) {
+    at::Tensor partial =
+        at::empty({mv_bias_gelu_partials(M, (int)N), N}, x.options().dtype(at::kFloat));
+    mv_bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), b.data_ptr(), dx.data_ptr(),
+                     partial.data_ptr<float>(), db.data_ptr(), M, (int)N, cur_stream());
+  }
+  return {dx, db};
+}
+
+std::vector<at::Tensor> ln_fwd(at::Tensor z, c10::optional<at::Tensor> bias,
+                               c10::optional<at::Tensor> res, at::Tensor gamma, at::Tensor beta,
+                               double eps, double p_drop, int64_t seed, bool save_v) {
+  c10::DeviceGuard guard(z.device());
+  const int64_t H = gamma.numel(), M = H ? z.numel() / H : 0;
+  TORCH_CHECK(H % 8 == 0 && H <= 4096 && z.size(-1) == H,
+              "ln: hidden size must be a multiple of 8, <= 4096, and match the last dim");
+  check_rows(z, M, H, "z");
+  check_rows(gamma, 1, H, "gamma");
+  check_rows(beta, 1, H, "beta");
+  LnFwdParams p{};
+  p.z = z.data_ptr();
+  if (bias.has_value() && bias->defined()) {
+    check_rows(*bias, 1, H, "bias");
+    p.bias = bias->data_ptr();
+  }
+  if (res.has_value() && res->defined()) {
+    check_rows(*res, M, H, "residual");
+    p.res = res->data_ptr();
+  }
+  p.gamma = gamma.data_ptr();
+  p.beta = beta.data_ptr();
+  at::Tensor y = at::empty_like(z);
+  at::Tensor v;
+  // without dropout/bias/residual the pre-LN value is z itself
+  const bool v_is_z = !p.bias && !p.res && p_drop == 0.0;
+  if (save_v) v = v_is_z ? z : at::empty_like(z);
+  auto fo = z.options().dtype(at::kFloat);
+  at::Tensor mean = at::empty({M}, fo), rstd = at::empty({M}, fo);
+  p.v = (save_v && !v_is_z) ? v.data_ptr() : nullptr;
+  p.y = y.data_ptr();
+  p.mean = mean.data_ptr<float>();
+  p.rstd = rstd.data_ptr<float>();
+  p.M = M;
+  p.H = (int)H;
+  p.eps = (float)eps;
+  p.p_drop = (float)p_drop;
+  p.seed = (uint32_t)seed;
+  p.thresh = drop_thresh(p_drop);
+  if (M) mv_ln_fwd(p, cur_stream());
+  return {y, v, mean, rstd};
+}
+
+// -> {dv, dz (undefined when p_drop == 0: equals dv), dgamma, dbeta, dbias}
+std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor v, at::Tensor mean, at::Tensor rstd,
+                               at::Tensor gamma, double p_drop, int64_t seed, bool need_dbias) {
+  c10::DeviceGuard guard(dy.device());
+  const int64_t H = gamma.numel(), M = H ? dy.numel() / H : 0;
+  TORCH_CHECK(H % 8 == 0 && H <= 4096, "ln: hidden size must be a multiple of 8, <= 4096");
+  check_rows(dy, M, H, "dy");
+  check_rows(v, M, H, "v");
+  check_rows(gamma, 1, H, "gamma");
+  TORCH_CHECK(mean.numel() == M && rstd.numel() == M && mean.scalar_type() == at::kFloat &&
+              rstd.scalar_type() == at::kFloat, "ln_bwd: mean/rstd must be fp32 [M]");
+  at::Tensor dv = at::empty_like(dy);
+  at::Tensor dz = p_drop > 0.0 ? at::empty_like(dy) : at::Tensor();
+  at::Tensor dg = at::zeros_like(gamma), db = at::zeros_like(gamma);
+  at::Tensor dbias = need_dbias ? at::zeros_like(gamma) : at::Tensor();
+  if (M) {
+    at::Tensor partial = at::empty({mv_ln_partials(M), 3, H}, dy.options().dtype(at::kFloat));
+    LnBwdParams p{};
+    p.dy = dy.data_ptr();
+    p.v = v.data_ptr();
+    p.mean = mean.data_ptr<float>();
+    p.rstd = rstd.data_ptr<float>();
+    p.gamma = gamma.data_ptr();
+    p.dv = dv.data_ptr();
+    p.dz = dz.defined() ? dz.data_ptr() : nullptr;
+    p.partial = partial.data_ptr<float>();
+    p.M = M;
+    p.H = (int)H;
+    p.p_drop = (float)p_drop;
+    p.seed = (uint32_t)seed;
+    p.thresh = drop_thresh(p_drop);
+    mv_ln_bwd(p, dg.data_ptr(), db.data_ptr(), need_dbias ? dbias.data_ptr() : nullptr,
+              cur_stream());
+  }
+  return {dv, dz, dg, db, dbias};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -441,6 +565,10 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("attn_fwd", &attn_fwd, "fused MFMA attention forward -> (out [b,s,h,64], lse)");
   m.def("attn_bwd", &attn_bwd, "fused MFMA attention backward -> dqkv");
   m.def("attn_dropout_mask", &attn_dropout_mask, "dropout keep-mask of the fused attention");
+  m.def("bias_gelu_fwd", &bias_gelu_fwd, "y = gelu(x + b) (erf form)");
+  m.def("bias_gelu_bwd", &bias_gelu_bwd, "-> (dx, dbias) of y = gelu(x + b)");
+  m.def("ln_fwd", &ln_fwd, "v = res + dropout(z + b); y = LN(v) -> (y, v, mean, rstd)");
+  m.def("ln_bwd", &ln_bwd, "-> (dv, dz, dgamma, dbeta, dbias)");
   m.def("bn_fwd_train", &bn_fwd_train, "fused NHWC BN(+add)(+ReLU) training forward");
   m.def("bn_apply", &bn_apply, "NHWC y = act(x*scale + bias (+res))");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward");

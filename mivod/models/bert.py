@@ -7,7 +7,8 @@ live in mivod's fused optimizer), Q/K/V as one [3H, H] projection GEMM, the
 MLM head evaluated only on the masked positions (the MLPerf/NVIDIA trick: the
 vocab GEMM shrinks ~6x at 15% masking), no torch.compile / Triton — the GEMMs
 are hipBLASLt via torch.matmul, attention is mivod's own path
-(``mivod.ops.attention``).
+(``mivod.ops.attention``), and every bias / GELU / dropout / residual /
+LayerNorm chain is one fused kernel each way (``mivod.ops.transformer``).
 """
 from __future__ import annotations
 
@@ -17,6 +18,8 @@ from dataclasses import dataclass
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ..ops.transformer import bias_dropout_add_ln, bias_gelu
 
 
 @dataclass
@@ -64,7 +67,7 @@ class BertEmbeddings(nn.Module):
         pos = torch.arange(s, device=input_ids.device)
         x = self.word_embeddings(input_ids) + self.position_embeddings(pos)[None] + \
             self.token_type_embeddings(token_type_ids)
-        return self.dropout(self.LayerNorm(x))
+        return self.dropout(bias_dropout_add_ln(x, None, None, self.LayerNorm))
 
 
 class BertSelfAttention(nn.Module):
@@ -83,7 +86,9 @@ class BertSelfAttention(nn.Module):
         b, s, hd = x.shape
         qkv = self.qkv(x).view(b, s, 3, self.h, self.d)
         ctx = attention(qkv, mask_bias, self.p_attn if self.training else 0.0)   # [b, s, h*d]
-        return self.LayerNorm(x + self.dropout(self.dense(ctx)))
+        # dense GEMM without bias; bias + dropout + residual + LayerNorm fused
+        return bias_dropout_add_ln(F.linear(ctx, self.dense.weight), self.dense.bias, x,
+                                   self.LayerNorm, self.dropout.p, self.training)
 
 
 class BertLayer(nn.Module):
@@ -97,8 +102,9 @@ class BertLayer(nn.Module):
 
     def forward(self, x, mask_bias):
         a = self.attention(x, mask_bias)
-        h = F.gelu(self.intermediate(a))
-        return self.LayerNorm(a + self.dropout(self.output(h)))
+        h = bias_gelu(F.linear(a, self.intermediate.weight), self.intermediate.bias)
+        return bias_dropout_add_ln(F.linear(h, self.output.weight), self.output.bias, a,
+                                   self.LayerNorm, self.dropout.p, self.training)
 
 
 class BertModel(nn.Module):
@@ -153,7 +159,8 @@ class BertForPreTraining(nn.Module):
         b, m = masked_positions.shape
         idx = masked_positions + torch.arange(b, device=seq.device)[:, None] * seq.shape[1]
         sel = seq.reshape(-1, seq.shape[-1]).index_select(0, idx.reshape(-1))
-        t = self.transform_ln(F.gelu(self.transform(sel)))
+        t = bias_dropout_add_ln(bias_gelu(F.linear(sel, self.transform.weight),
+                                          self.transform.bias), None, None, self.transform_ln)
         logits = F.linear(t, self.bert.embeddings.word_embeddings.weight, self.decoder_bias)
         mlm = F.cross_entropy(logits.float(), masked_labels.reshape(-1), ignore_index=-100)
         nsp = F.cross_entropy(self.nsp(pooled).float(), nsp_labels)

@@ -17,6 +17,7 @@ run() {  # run <name> <timeout> <cmd...>
 }
 for v in ${VARIANTS:-default}; do
   case $v in
+    tests_sel) run pytest_sel 900 python -m pytest ${TESTS_SEL:-tests} -m gpu -q ;;
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
     default) run bench_default 1200 python bench.py --steps 20 --warmup 10 ;;
     normal) MIOPEN_FIND_MODE=NORMAL run bench_normal 1200 python bench.py --steps 20 --warmup 10 ;;

@@ -1,0 +1,122 @@
+"""Fused transformer elementwise kernels (mv_bert.hip) vs fp32 PyTorch references:
+bias+GELU forward/backward (incl. the fused bias-grad column sums) and
+bias+dropout+residual+LayerNorm forward/backward (dgamma/dbeta/dbias), odd
+widths and row counts, dropout with the kernels' counter-hash mask, and a BERT
+training step fused vs eager."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mivod.ops import kernels as K
+from mivod.ops.transformer import _BiasDropoutAddLN, _BiasGelu, dropout_keep_mask
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N", [(256, 4096), (111, 1024), (64, 1000), (33, 4104), (4096, 64)])
+def test_bias_gelu_matches_reference(cuda, M, N):
+    torch.manual_seed(0)
+    x = (torch.randn(M, N, device=cuda) * 2).to(torch.bfloat16)
+    b = (torch.randn(N, device=cuda) * 0.5).to(torch.bfloat16)
+    dy = torch.randn(M, N, device=cuda).to(torch.bfloat16)
+    xg, bg = x.clone().requires_grad_(), b.clone().requires_grad_()
+    y = _BiasGelu.apply(xg, bg)
+    y.backward(dy)
+    xr, br = x.float().requires_grad_(), b.float().requires_grad_()
+    yr = F.gelu(xr + br)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(xg.grad.float(), xr.grad, rtol=2e-2, atol=2e-2)
+    # column sums of M bf16-rounded terms: tolerance scales with sqrt(M)
+    torch.testing.assert_close(bg.grad.float(), br.grad, rtol=2e-2, atol=0.05 * M ** 0.5)
+
+
+def _ln_ref(z, bias, res, gamma, beta, eps, keep, p):
+    t = z.float()
+    if bias is not None:
+        t = t + bias.float()
+    if keep is not None:
+        t = t * keep.float() / (1.0 - p)
+    if res is not None:
+        t = t + res.float()
+    return F.layer_norm(t, (z.shape[-1],), gamma.float(), beta.float(), eps)
+
+
+@pytest.mark.parametrize("M,H", [(512, 1024), (77, 768), (256, 64), (40, 4096), (64, 1032)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("with_bias_res", [True, False])
+def test_bias_dropout_add_ln_matches_reference(cuda, M, H, p, with_bias_res):
+    torch.manual_seed(1)
+    bf = torch.bfloat16
+    z = torch.randn(M, H, device=cuda).to(bf)
+    bias = (torch.randn(H, device=cuda) * 0.3).to(bf) if with_bias_res else None
+    res = torch.randn(M, H, device=cuda).to(bf) if with_bias_res else None
+    gamma = (1 + 0.2 * torch.randn(H, device=cuda)).to(bf)
+    beta = (0.1 * torch.randn(H, device=cuda)).to(bf)
+    dy = torch.randn(M, H, device=cuda).to(bf)
+    eps, seed = 1e-12, 4321
+    keep = dropout_keep_mask(M, H, p, seed, cuda) if p > 0 else None
+    if keep is not None:
+        assert abs((1 - keep.float().mean().item()) - p) < 0.02
+
+    leaves = [t.clone().requires_grad_() if t is not None else None
+              for t in (z, bias, res, gamma, beta)]
+    y = _BiasDropoutAddLN.apply(leaves[0], leaves[1], leaves[2], leaves[3], leaves[4], eps, p,
+                                seed)
+    y.backward(dy)
+    refs = [t.float().requires_grad_() if t is not None else None
+            for t in (z, bias, res, gamma, beta)]
+    yr = _ln_ref(*refs, eps, keep, p)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    for got, ref, name in zip(leaves, refs, ("z", "bias", "res", "gamma", "beta")):
+        if got is None:
+            continue
+        tol = 0.05 * M ** 0.5 if name in ("bias", "gamma", "beta") else 5e-2
+        torch.testing.assert_close(got.grad.float(), ref.grad, rtol=3e-2, atol=tol,
+                                   msg=lambda m: f"{name}: {m}")
+
+
+def test_ln_no_bias_no_res_saves_input_as_v(cuda):
+    z = torch.randn(64, 1024, device=cuda).to(torch.bfloat16)
+    g = torch.ones(1024, device=cuda, dtype=torch.bfloat16)
+    b = torch.zeros(1024, device=cuda, dtype=torch.bfloat16)
+    y, v, mean, rstd = K.native().ln_fwd(z, None, None, g, b, 1e-5, 0.0, 0, True)
+    assert v.data_ptr() == z.data_ptr()
+    torch.testing.assert_close(mean, z.float().mean(-1), rtol=1e-4, atol=1e-4)
+
+
+def test_ln_deterministic(cuda):
+    torch.manual_seed(2)
+    z = torch.randn(1000, 1024, device=cuda).to(torch.bfloat16)
+    g = torch.ones(1024, device=cuda, dtype=torch.bfloat16)
+    b = torch.zeros(1024, device=cuda, dtype=torch.bfloat16)
+    dy = torch.randn_like(z)
+    y, v, mean, rstd = K.native().ln_fwd(z, g, z, g, b, 1e-5, 0.1, 7, True)
+    outs = [K.native().ln_bwd(dy, v, mean, rstd, g, 0.1, 7, True) for _ in range(2)]
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+
+
+def test_bert_step_fused_matches_eager(cuda, monkeypatch):
+    from mivod.models.bert import BertConfig, BertForPreTraining, synthetic_batch
+    c = BertConfig.tiny(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    torch.manual_seed(3)
+    model = BertForPreTraining(c).to(cuda).to(torch.bfloat16)
+    batch = synthetic_batch(c, 4, 64, cuda)
+    grads = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MIVOD_FUSED_TRANSFORMER", fused)
+        model.zero_grad(set_to_none=True)
+        loss = model(*batch)
+        loss.backward()
+        grads[fused] = (loss.item(), {n: p.grad.float().clone()
+                                      for n, p in model.named_parameters()
+                                      if p.grad is not None})
+    (l1, g1), (l0, g0) = grads["1"], grads["0"]
+    assert abs(l1 - l0) < 0.02 * abs(l0) + 1e-2
+    assert g1.keys() == g0.keys()
+    for n in g0:
+        scale = g0[n].abs().max().item() + 1e-6
+        err = (g1[n] - g0[n]).abs().max().item()
+        assert err <= 0.1 * scale + 1e-3, (n, err, scale)
