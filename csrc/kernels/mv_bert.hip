@@ -97,36 +97,40 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const __bf16* __rest
   for (int j = 0; j < 8; ++j) partial[(int64_t)blockIdx.x * N + c + j] = acc[j];
 }
 
-// column sums of [P][N] partials (fixed order) -> bf16 / fp32 output
+// Column sums of fp32 partials -> bf16.  Partial row p of set `y` lives at
+// partial + y*set_off + p*stride.  A workgroup owns 16 columns x 16 row groups
+// (64 B coalesced per row, >= 192 workgroups for BERT's shapes); the 16 group
+// sums combine through LDS in a fixed order: deterministic.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ partial, int P,
-                                                      int N, __bf16* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= N) return;
+                                                      int N, int64_t stride, int64_t set_off,
+                                                      __bf16* __restrict__ out0,
+                                                      __bf16* __restrict__ out1,
+                                                      __bf16* __restrict__ out2) {
+  __bf16* out = blockIdx.y == 0 ? out0 : (blockIdx.y == 1 ? out1 : out2);
+  if (!out) return;                                    // uniform per workgroup
+  const int tc = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + tc;
+  const float* base = partial + blockIdx.y * set_off + c;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int p = 0;
-  for (; p + 3 < P; p += 4) {
-    s0 += partial[(int64_t)p * N + c];
-    s1 += partial[(int64_t)(p + 1) * N + c];
-    s2 += partial[(int64_t)(p + 2) * N + c];
-    s3 += partial[(int64_t)(p + 3) * N + c];
+  if (c < N) {
+    int p = g;
+    for (; p + 48 < P; p += 64) {
+      s0 += base[(int64_t)p * stride];
+      s1 += base[(int64_t)(p + 16) * stride];
+      s2 += base[(int64_t)(p + 32) * stride];
+      s3 += base[(int64_t)(p + 48) * stride];
+    }
+    for (; p < P; p += 16) s0 += base[(int64_t)p * stride];
   }
-  for (; p < P; ++p) s0 += partial[(int64_t)p * N + c];
-  out[c] = (__bf16)((s0 + s1) + (s2 + s3));
-}
-
-__global__ __launch_bounds__(256) void colsum_strided_kernel(const float* __restrict__ partial,
-                                                              int P, int N, int64_t stride,
-                                                              __bf16* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= N) return;
-  float s0 = 0.f, s1 = 0.f;
-  int p = 0;
-  for (; p + 1 < P; p += 2) {
-    s0 += partial[(int64_t)p * stride + c];
-    s1 += partial[(int64_t)(p + 1) * stride + c];
+  __shared__ float red[16][17];
+  red[g][tc] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && c < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][tc];
+    out[c] = (__bf16)t;
   }
-  if (p < P) s0 += partial[(int64_t)p * stride + c];
-  out[c] = (__bf16)(s0 + s1);
 }
 
 // ------------------------------------------------- bias + dropout + add + LN
@@ -344,8 +348,9 @@ void mv_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, fl
   hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3((unsigned)P, (N + 2047) / 2048), dim3(256), 0, st,
                      (const __bf16*)dy, (const __bf16*)x, (const __bf16*)b, (__bf16*)dx, partial,
                      M, N, rpb);
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256), dim3(256), 0, st,
-                     (const float*)partial, (int)P, N, (__bf16*)dbias);
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 15) / 16, 1), dim3(256), 0, st,
+                     (const float*)partial, (int)P, N, (int64_t)N, (int64_t)0, (__bf16*)dbias,
+                     (__bf16*)nullptr, (__bf16*)nullptr);
 }
 
 int64_t mv_ln_partials(int64_t M) { return (M + kRowsPerBlock - 1) / kRowsPerBlock; }
@@ -370,12 +375,8 @@ void mv_ln_bwd(const LnBwdParams& p, void* dgamma, void* dbeta, void* dbias, hip
   else if (p.H <= 1024) hipLaunchKernelGGL(ln_bwd_kernel<2>, g, dim3(256), 0, st, a);
   else if (p.H <= 2048) hipLaunchKernelGGL(ln_bwd_kernel<4>, g, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ln_bwd_kernel<8>, g, dim3(256), 0, st, a);
-  // partial layout [P][3][H]: column sums with row stride 3H, one launch each
-  void* outs[3] = {dgamma, dbeta, dbias};
-  for (int w = 0; w < 3; ++w) {
-    if (!outs[w]) continue;
-    hipLaunchKernelGGL(colsum_strided_kernel, dim3((p.H + 255) / 256), dim3(256), 0, st,
-                       (const float*)p.partial + (int64_t)w * p.H, (int)P, p.H, 3 * p.H,
-                       (__bf16*)outs[w]);
-  }
+  // partial layout [P][3][H]: set stride H, row stride 3H; one launch for all three
+  hipLaunchKernelGGL(colsum_kernel, dim3((p.H + 15) / 16, 3), dim3(256), 0, st,
+                     (const float*)p.partial, (int)P, p.H, (int64_t)3 * p.H, (int64_t)p.H,
+                     (__bf16*)dgamma, (__bf16*)dbeta, (__bf16*)dbias);
 }

@@ -453,7 +453,7 @@ std::vector<at::Tensor> bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor b)
   check_rows(dy, M, N, "dy");
   check_rows(b, 1, N, "bias");
   at::Tensor dx = at::empty_like(x);
-  at::Tensor db = at::zeros_like(b);
+  at::Tensor db = M ? at::empty_like(b) : at::zeros_like(b);
   if (M) {
     at::Tensor partial =
         at::empty({mv_bias_gelu_partials(M, (int)N), N}, x.options().dtype(at::kFloat));
@@ -519,8 +519,10 @@ std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor v, at::Tensor mean, at:
               rstd.scalar_type() == at::kFloat, "ln_bwd: mean/rstd must be fp32 [M]");
   at::Tensor dv = at::empty_like(dy);
   at::Tensor dz = p_drop > 0.0 ? at::empty_like(dy) : at::Tensor();
-  at::Tensor dg = at::zeros_like(gamma), db = at::zeros_like(gamma);
-  at::Tensor dbias = need_dbias ? at::zeros_like(gamma) : at::Tensor();
+  // every column sum is written by the finalize kernel when M > 0
+  auto alloc = [&]() { return M ? at::empty_like(gamma) : at::zeros_like(gamma); };
+  at::Tensor dg = alloc(), db = alloc();
+  at::Tensor dbias = need_dbias ? alloc() : at::Tensor();
   if (M) {
     at::Tensor partial = at::empty({mv_ln_partials(M), 3, H}, dy.options().dtype(at::kFloat));
     LnBwdParams p{};
