@@ -23,6 +23,12 @@ import sys
 import time
 
 os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+# MIOpen's naive direct-conv fallbacks are never competitive on gfx950, and their
+# kernels are not kept in the kernel cache, which invalidates every find-db record
+# that lists them: Find then re-runs on each fresh process (~115 s at bs512,
+# benchmarking 50-150 ms naive kernels).  Keep them out of the search.
+for _d in ("FWD", "BWD", "WRW"):
+    os.environ.setdefault(f"MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_{_d}", "0")
 # Ship MIOpen's find-db + compiled-kernel cache with the repo (.miopen/): a fresh
 # MI355X box otherwise spends ~3 minutes JIT-compiling ResNet-50's conv kernels.
 _MIO = os.path.join(os.path.dirname(os.path.abspath(__file__)), ".miopen")
@@ -37,7 +43,10 @@ if os.path.isdir(_MIO) and "MIOPEN_USER_DB_PATH" not in os.environ:
         if os.path.isdir(src):
             for f in os.listdir(src):
                 if not os.path.exists(os.path.join(dst, f)):
-                    shutil.copy2(os.path.join(src, f), os.path.join(dst, f))
+                    # copy + atomic rename: the ranks of one node share this dir
+                    part = os.path.join(dst, f".{f}.{os.getpid()}.part")
+                    shutil.copy2(os.path.join(src, f), part)
+                    os.replace(part, os.path.join(dst, f))
         os.environ.setdefault(var, dst)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 

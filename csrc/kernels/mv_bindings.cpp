@@ -14,6 +14,7 @@
 #include "mv_bert.h"
 #include "mv_bn.h"
 #include "mv_kernels.h"
+#include "mv_pool.h"
 
 namespace {
 
@@ -311,10 +312,34 @@ at::Tensor bn_apply(at::Tensor x, at::Tensor scale, at::Tensor bias, bool relu,
   return y;
 }
 
+// statistics only: running-stat update + saved {mean, invstd, scale, bias}; no apply pass
+at::Tensor bn_stats(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
+                    c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
+                    double momentum, double eps) {
+  int64_t C;
+  const int64_t M = bn_check_act(x, "x", &C);
+  TORCH_CHECK(M > 0, "bn: empty input");
+  c10::DeviceGuard guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  const int P = mv_bn_partials(M, (int)C);
+  at::Tensor partial = at::empty({(int64_t)P * 2 * C}, fo);
+  at::Tensor vec = at::empty({4, C}, fo);
+  float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
+  float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "bn: running_mean/var must both be given");
+  mv_bn_fwd_train(x.data_ptr(), nullptr, nullptr, M, (int)C, rm, rv, opt_f32(gamma, C, "weight"),
+                  opt_f32(beta, C, "bias"), (float)momentum, (float)eps, false,
+                  partial.data_ptr<float>(), P, vec[0].data_ptr<float>(),
+                  vec[1].data_ptr<float>(), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
+                  cur_stream());
+  return vec;
+}
+
 // returns {dx, dgamma, dbeta, dz}; dz defined only for mode 2 (residual branch grad)
 std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
                                c10::optional<at::Tensor> y, at::Tensor vec,
-                               c10::optional<at::Tensor> gamma, bool need_affine_grad) {
+                               c10::optional<at::Tensor> gamma, bool need_affine_grad,
+                               c10::optional<at::Tensor> dy2) {
   int64_t C, C2;
   const int64_t M = bn_check_act(x, "x", &C);
   bn_check_act(dy, "grad", &C2);
@@ -329,6 +354,14 @@ std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
                 "bn: mode 2 needs the saved output");
     yp = y->data_ptr();
   }
+  const void* dy2p = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    TORCH_CHECK(mode == 2, "bn: a second gradient stream is supported for mode 2 only");
+    TORCH_CHECK(dy2->sizes() == x.sizes() && dy2->strides() == x.strides() &&
+                dy2->scalar_type() == at::kBFloat16 && dy2->is_cuda(),
+                "bn: dy2 must match x in shape, layout and dtype");
+    dy2p = dy2->data_ptr();
+  }
   c10::DeviceGuard guard(x.device());
   auto fo = x.options().dtype(at::kFloat);
   const int P = mv_bn_partials(M, (int)C);
@@ -337,7 +370,7 @@ std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
   at::Tensor dx = at::empty_like(x);
   at::Tensor dz;
   if (mode == 2) dz = at::empty_like(x);
-  mv_bn_bwd((int)mode, dy.data_ptr(), x.data_ptr(), yp, mode == 2 ? dz.data_ptr() : nullptr,
+  mv_bn_bwd((int)mode, dy.data_ptr(), dy2p, x.data_ptr(), yp, mode == 2 ? dz.data_ptr() : nullptr,
             dx.data_ptr(), M, (int)C, vec[0].data_ptr<float>(), vec[1].data_ptr<float>(),
             opt_f32(gamma, C, "weight"), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
             work[0].data_ptr<float>(), work[1].data_ptr<float>(), partial.data_ptr<float>(), P,
@@ -545,6 +578,78 @@ std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor v, at::Tensor mean, at:
   return {dv, dz, dg, db, dbias};
 }
 
+// ---------------------------------------------------------------------------
+// NHWC pooling
+// ---------------------------------------------------------------------------
+void check_nhwc(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4 &&
+              t.is_contiguous(at::MemoryFormat::ChannelsLast) && t.size(1) % 8 == 0,
+              "pool: ", what, " must be a channels_last bf16 GPU tensor with C % 8 == 0");
+}
+
+std::vector<at::Tensor> maxpool_fwd(at::Tensor x, c10::optional<at::Tensor> scale,
+                                    c10::optional<at::Tensor> bias, bool relu, int64_t k,
+                                    int64_t s, int64_t p) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(k >= 1 && k * k <= 255 && s >= 1 && p >= 0 && 2 * p <= k, "maxpool: bad window");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "maxpool: empty output");
+  const float* sp = nullptr;
+  const float* bp = nullptr;
+  if (scale.has_value() && scale->defined()) {
+    TORCH_CHECK(bias.has_value() && bias->defined(), "maxpool: scale needs bias");
+    sp = opt_f32(scale, C, "scale");
+    bp = opt_f32(bias, C, "bias");
+  }
+  c10::DeviceGuard guard(x.device());
+  at::Tensor y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor idx = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  mv_maxpool_fwd(x.data_ptr(), sp, bp, relu, y.data_ptr(), idx.data_ptr<uint8_t>(), (int)N,
+                 (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p, cur_stream());
+  return {y, idx};
+}
+
+at::Tensor maxpool_bwd(at::Tensor dy, c10::optional<at::Tensor> dy2, at::Tensor idx, int64_t H,
+                       int64_t W, int64_t k, int64_t s, int64_t p) {
+  check_nhwc(dy, "dy");
+  const int64_t N = dy.size(0), C = dy.size(1), OH = dy.size(2), OW = dy.size(3);
+  TORCH_CHECK(OH == (H + 2 * p - k) / s + 1 && OW == (W + 2 * p - k) / s + 1,
+              "maxpool_bwd: output size does not match the window");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.is_contiguous() &&
+              idx.numel() == dy.numel(), "maxpool_bwd: idx must be uint8 [N, OH, OW, C]");
+  const void* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    check_nhwc(*dy2, "dy2");
+    TORCH_CHECK(dy2->sizes() == dy.sizes(), "maxpool_bwd: dy2 shape");
+    d2 = dy2->data_ptr();
+  }
+  c10::DeviceGuard guard(dy.device());
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  mv_maxpool_bwd(dy.data_ptr(), d2, idx.data_ptr<uint8_t>(), dx.data_ptr(), (int)N, (int)H, (int)W,
+                 (int)C, (int)OH, (int)OW, (int)k, (int)s, (int)p, cur_stream());
+  return dx;
+}
+
+at::Tensor gap_fwd(at::Tensor x) {
+  check_nhwc(x, "x");
+  c10::DeviceGuard guard(x.device());
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  at::Tensor y = at::empty({N, C}, x.options());
+  mv_gap_fwd(x.data_ptr(), y.data_ptr(), (int)N, (int)HW, (int)C, cur_stream());
+  return y;
+}
+
+at::Tensor gap_bwd(at::Tensor dy, int64_t H, int64_t W) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 2 &&
+              dy.is_contiguous() && dy.size(1) % 8 == 0, "gap_bwd: dy must be bf16 [N, C]");
+  c10::DeviceGuard guard(dy.device());
+  const int64_t N = dy.size(0), C = dy.size(1);
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  mv_gap_bwd(dy.data_ptr(), dx.data_ptr(), (int)N, (int)(H * W), (int)C, cur_stream());
+  return dx;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -573,5 +678,10 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("ln_bwd", &ln_bwd, "-> (dv, dz, dgamma, dbeta, dbias)");
   m.def("bn_fwd_train", &bn_fwd_train, "fused NHWC BN(+add)(+ReLU) training forward");
   m.def("bn_apply", &bn_apply, "NHWC y = act(x*scale + bias (+res))");
-  m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward");
+  m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward (+ second grad stream)");
+  m.def("bn_stats", &bn_stats, "NHWC BN training statistics only -> [4, C]");
+  m.def("maxpool_fwd", &maxpool_fwd, "NHWC maxpool with fused affine+ReLU prologue -> (y, idx)");
+  m.def("maxpool_bwd", &maxpool_bwd, "NHWC maxpool backward (gather, + second grad stream)");
+  m.def("gap_fwd", &gap_fwd, "NHWC global average pool -> [N, C]");
+  m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
 }

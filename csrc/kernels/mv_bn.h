@@ -6,6 +6,7 @@
 // number of row-partials the reduction passes produce (size the [P][2][C] workspace)
 int mv_bn_partials(int64_t M, int C);
 
+// y == nullptr: statistics + running-stat update + scale/bias only (no apply pass)
 void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, float* rmean,
                      float* rvar, const float* gamma, const float* beta, float momentum, float eps,
                      bool relu, float* partial, int P, float* save_mean, float* save_invstd,
@@ -14,8 +15,9 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
 void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
                  const float* bias, bool relu, hipStream_t st);
 
-// mode 0: plain BN, 1: BN+ReLU (mask from x), 2: BN+add+ReLU (mask from y, writes dz)
-void mv_bn_bwd(int mode, const void* dy, const void* x, const void* y, void* dz, void* dx,
+// mode 0: plain BN, 1: BN+ReLU (mask from x), 2: BN+add+ReLU (mask from y, writes dz).
+// dy2 (mode 2 only, may be null): second gradient stream added to dy on the fly.
+void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const void* y, void* dz, void* dx,
                int64_t M, int C, const float* save_mean, const float* save_invstd,
                const float* gamma, const float* scale, const float* bias, float* dgamma,
                float* dbeta, float* partial, int P, float* ca, float* cb, float* cc,

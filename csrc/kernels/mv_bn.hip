@@ -249,7 +249,8 @@ __device__ __forceinline__ void masked(const float (&dy)[8], const float (&x)[8]
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
-    const __bf16* __restrict__ dy, const __bf16* __restrict__ x, const __bf16* __restrict__ y,
+    const __bf16* __restrict__ dy, const __bf16* __restrict__ dy2, const __bf16* __restrict__ x,
+    const __bf16* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ scale,
     const float* __restrict__ bias, __bf16* __restrict__ dz, float* __restrict__ partial, Geo g) {
   int tc, tr, c;
@@ -269,6 +270,13 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
       const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
       load8(dy + o0, a0);
       load8(dy + o1, a1);
+      if (dy2) {   // second gradient stream of a tapped output (uniform branch)
+        float b0[8], b1[8];
+        load8(dy2 + o0, b0);
+        load8(dy2 + o1, b1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a0[j] += b0[j]; a1[j] += b1[j]; }
+      }
       load8(x + o0, x0);
       load8(x + o1, x1);
       if (MODE == 2) { load8(y + o0, y0); load8(y + o1, y1); }
@@ -285,6 +293,12 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
       float a0[8], x0[8], y0[8], d0[8];
       const int64_t o0 = r * g.C + c;
       load8(dy + o0, a0);
+      if (dy2) {
+        float b0[8];
+        load8(dy2 + o0, b0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a0[j] += b0[j];
+      }
       load8(x + o0, x0);
       if (MODE == 2) load8(y + o0, y0);
       masked<MODE>(a0, x0, y0, sc, bi, d0);
@@ -446,7 +460,7 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
   hipLaunchKernelGGL(finalize_fwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
                      partial, (int)grr.x, M, C, rmean, rvar, gamma, beta, momentum, eps, save_mean,
                      save_invstd, scale, bias);
-  mv_bn_apply(x, res, y, M, C, scale, bias, relu, st);
+  if (y) mv_bn_apply(x, res, y, M, C, scale, bias, relu, st);   // y == null: statistics only
 }
 
 void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
@@ -465,7 +479,7 @@ void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, cons
   }
 }
 
-void mv_bn_bwd(int mode, const void* dy, const void* x, const void* y, void* dz, void* dx,
+void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const void* y, void* dz, void* dx,
                int64_t M, int C, const float* save_mean, const float* save_invstd,
                const float* gamma, const float* scale, const float* bias, float* dgamma,
                float* dbeta, float* partial, int P, float* ca, float* cb, float* cc,
@@ -473,13 +487,14 @@ void mv_bn_bwd(int mode, const void* dy, const void* x, const void* y, void* dz,
   Geo gr = reduce_geo(M, C, P);
   dim3 grr = grid_of(gr);
   const __bf16* dyp = (const __bf16*)dy;
+  const __bf16* dy2p = (const __bf16*)dy2;
   const __bf16* xp = (const __bf16*)x;
   const __bf16* yp = (const __bf16*)y;
   __bf16* dzp = (__bf16*)dz;
   switch (mode) {
-    case 0: hipLaunchKernelGGL((bwd_reduce_kernel<0>), grr, dim3(kBlock), 0, st, dyp, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
-    case 1: hipLaunchKernelGGL((bwd_reduce_kernel<1>), grr, dim3(kBlock), 0, st, dyp, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
-    default: hipLaunchKernelGGL((bwd_reduce_kernel<2>), grr, dim3(kBlock), 0, st, dyp, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
+    case 0: hipLaunchKernelGGL((bwd_reduce_kernel<0>), grr, dim3(kBlock), 0, st, dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
+    case 1: hipLaunchKernelGGL((bwd_reduce_kernel<1>), grr, dim3(kBlock), 0, st, dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
+    default: hipLaunchKernelGGL((bwd_reduce_kernel<2>), grr, dim3(kBlock), 0, st, dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
   }
   hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
                      partial, (int)grr.x, M, C, save_mean, save_invstd, gamma, dgamma, dbeta, ca,

@@ -1,0 +1,13 @@
+// NHWC pooling kernels (mv_pool.hip): fused affine+ReLU+maxpool with uint8
+// argmax, gather-form maxpool backward, global average pool fwd/bwd.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+void mv_maxpool_fwd(const void* x, const float* scale, const float* bias, bool relu, void* y,
+                    uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int k, int s, int p,
+                    hipStream_t st);
+void mv_maxpool_bwd(const void* dy, const void* dy2, const uint8_t* idx, void* dx, int N, int H,
+                    int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st);
+void mv_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
+void mv_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);

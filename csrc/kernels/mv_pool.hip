@@ -1,0 +1,213 @@
+// NHWC pooling kernels for the ResNet stem / head on gfx950.
+//
+//  * maxpool_fwd: y = maxpool_kxk/s(act(x)) with an optional fused per-channel
+//    affine + ReLU prologue (the stem's BatchNorm apply), argmax stored as one
+//    uint8 per output element (window position, k*k <= 255).  torch's NHWC
+//    max-pool writes int64 indices (8 B per output element) and needs the BN
+//    output materialised first: for ResNet-50 bs512 that is an 822 MB write +
+//    read + an 822 MB index write that this kernel never does.
+//  * maxpool_bwd: gather form — each input element sums the (<= ceil(k/s)^2)
+//    output gradients whose argmax points at it.  No zero-fill, no atomics,
+//    deterministic; optional second gradient stream dy2 (tapped output).
+//  * gap_fwd / gap_bwd: global average pool over H*W (NHWC) and its broadcast
+//    backward (torch's channels_last expand falls back to a non-vectorized
+//    elementwise kernel: 160 us per step at bs512).
+//
+// Every lane handles 8 consecutive channels of one pixel (16 B bf16 vectors);
+// C % 8 == 0 is checked on the host.
+#include "mv_common.h"
+#include "mv_pool.h"
+
+namespace mv {
+namespace pool {
+
+struct PoolGeo {
+  int N, H, W, C, OH, OW, k, s, p;
+};
+
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restrict__ x,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ bias,
+                                                          int relu, __bf16* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, PoolGeo g) {
+  const int cv = g.C / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)g.N * g.OH * g.OW * cv;
+  if (t >= total) return;
+  const int c = (int)(t % cv) * 8;
+  int64_t pix = t / cv;
+  const int ow = (int)(pix % g.OW);
+  pix /= g.OW;
+  const int oh = (int)(pix % g.OH);
+  const int n = (int)(pix / g.OH);
+  float sc[8], bi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = 1.f; bi[j] = 0.f; }
+  if (scale) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = scale[c + j]; bi[j] = bias[c + j]; }
+  }
+  float best[8];
+  uint32_t arg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+  const int h0 = oh * g.s - g.p, w0 = ow * g.s - g.p;
+  for (int kh = 0; kh < g.k; ++kh) {
+    const int ih = h0 + kh;
+    if (ih < 0 || ih >= g.H) continue;
+    for (int kw = 0; kw < g.k; ++kw) {
+      const int iw = w0 + kw;
+      if (iw < 0 || iw >= g.W) continue;
+      float v[8];
+      load8(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c, v);
+      const uint32_t pos = kh * g.k + kw;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = scale ? __builtin_fmaf(v[j], sc[j], bi[j]) : v[j];
+        if (relu) a = a > 0.f ? a : 0.f;
+        a = (float)(__bf16)a;                  // compare what torch would have stored
+        if (a > best[j] || __builtin_isnan(a)) {   // first maximum wins (torch order)
+          best[j] = a;
+          arg[j] = pos;
+        }
+      }
+    }
+  }
+  store8(y + t * 8, best);
+  uint32_t lo = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+  uint32_t hi = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  *reinterpret_cast<u32x2*>(idx + t * 8) = u32x2{lo, hi};
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restrict__ dy,
+                                                          const __bf16* __restrict__ dy2,
+                                                          const uint8_t* __restrict__ idx,
+                                                          __bf16* __restrict__ dx, PoolGeo g) {
+  const int cv = g.C / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)g.N * g.H * g.W * cv;
+  if (t >= total) return;
+  const int c = (int)(t % cv) * 8;
+  int64_t pix = t / cv;
+  const int iw = (int)(pix % g.W);
+  pix /= g.W;
+  const int ih = (int)(pix % g.H);
+  const int n = (int)(pix / g.H);
+  // output windows containing ih: oh*s - p <= ih <= oh*s - p + k - 1
+  const int ohl = max(0, (ih + g.p - g.k + g.s) / g.s);
+  const int ohh = min(g.OH - 1, (ih + g.p) / g.s);
+  const int owl = max(0, (iw + g.p - g.k + g.s) / g.s);
+  const int owh = min(g.OW - 1, (iw + g.p) / g.s);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int oh = ohl; oh <= ohh; ++oh) {
+    const int kh = ih - (oh * g.s - g.p);
+    if (kh < 0 || kh >= g.k) continue;
+    for (int ow = owl; ow <= owh; ++ow) {
+      const int kw = iw - (ow * g.s - g.p);
+      if (kw < 0 || kw >= g.k) continue;
+      const uint32_t pos = kh * g.k + kw;
+      const int64_t o = (((int64_t)n * g.OH + oh) * g.OW + ow) * g.C + c;
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 a = *reinterpret_cast<const u32x2*>(idx + o);
+      float d[8];
+      load8(dy + o, d);
+      if (dy2) {
+        float e[8];
+        load8(dy2 + o, e);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] += e[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t w = j < 4 ? a[0] : a[1];
+        const uint32_t id = (w >> (8 * (j & 3))) & 0xffu;
+        if (id == pos) acc[j] += d[j];
+      }
+    }
+  }
+  store8(dx + t * 8, acc);
+}
+
+// global average pool: x [N, HW, C] -> y [N, C]; one lane per (n, 8 channels)
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const __bf16* __restrict__ x,
+                                                      __bf16* __restrict__ y, int N, int HW,
+                                                      int C) {
+  const int cv = C / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)N * cv) return;
+  const int n = (int)(t / cv), c = (int)(t % cv) * 8;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  const __bf16* base = x + (int64_t)n * HW * C + c;
+  for (int i = 0; i < HW; ++i) {
+    float v[8];
+    load8(base + (int64_t)i * C, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += v[j];
+  }
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] *= inv;
+  store8(y + (int64_t)n * C + c, s);
+}
+
+// dx[n, i, c] = dy[n, c] / HW
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const __bf16* __restrict__ dy,
+                                                      __bf16* __restrict__ dx, int N, int HW,
+                                                      int C) {
+  const int cv = C / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)N * HW * cv) return;
+  const int c = (int)(t % cv) * 8;
+  const int n = (int)(t / ((int64_t)HW * cv));
+  float v[8];
+  load8(dy + (int64_t)n * C + c, v);
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= inv;
+  store8(dx + t * 8, v);
+}
+
+}  // namespace pool
+}  // namespace mv
+
+using namespace mv::pool;
+
+static unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+void mv_maxpool_fwd(const void* x, const float* scale, const float* bias, bool relu, void* y,
+                    uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int k, int s, int p,
+                    hipStream_t st) {
+  PoolGeo g{N, H, W, C, OH, OW, k, s, p};
+  const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  if (!total) return;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
+                     (const __bf16*)x, scale, bias, relu ? 1 : 0, (__bf16*)y, idx, g);
+}
+
+void mv_maxpool_bwd(const void* dy, const void* dy2, const uint8_t* idx, void* dx, int N, int H,
+                    int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st) {
+  PoolGeo g{N, H, W, C, OH, OW, k, s, p};
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  if (!total) return;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
+                     (const __bf16*)dy, (const __bf16*)dy2, idx, (__bf16*)dx, g);
+}
+
+void mv_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st) {
+  const int64_t total = (int64_t)N * (C / 8);
+  if (!total) return;
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st, (const __bf16*)x,
+                     (__bf16*)y, N, HW, C);
+}
+
+void mv_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st) {
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  if (!total) return;
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
+                     (const __bf16*)dy, (__bf16*)dx, N, HW, C);
+}

@@ -12,7 +12,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops.bn import BatchNorm2d
+from ..ops.bn import BatchNorm2d, bn_relu_maxpool, global_avg_pool, tap
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -35,12 +35,13 @@ class Bottleneck(nn.Module):
         self.bn2 = BatchNorm2d(planes)
         self.conv3 = conv1x1(planes, planes * self.expansion)
         self.bn3 = BatchNorm2d(planes * self.expansion)
-        if zero_init_residual:
-            nn.init.zeros_(self.bn3.weight)
         self.downsample = downsample
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
+        # the shortcut's gradient is added inside the backward of the op that
+        # produced x (mivod.ops.bn.tap), not by a separate autograd add
+        src = tap(x)
+        identity = src if self.downsample is None else self.downsample(src)
         out = self.bn1(self.conv1(x), relu=True)
         out = self.bn2(self.conv2(out), relu=True)
         # fused: relu(bn3(conv3(out)) + identity) in one pass (mivod.ops.bn)
@@ -66,6 +67,10 @@ class ResNet(nn.Module):
             elif isinstance(m, nn.BatchNorm2d):
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
+        if zero_init_residual:          # after the generic init, which would undo it
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
 
     def _make_layer(self, planes, blocks, stride, zir):
         down = None
@@ -79,10 +84,9 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x), relu=True))
+        x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)   # fused stem
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(self.avgpool(x), 1)
-        return self.fc(x)
+        return self.fc(global_avg_pool(x))
 
 
 def resnet50(num_classes=1000, **kw) -> ResNet:

@@ -9,6 +9,8 @@ takes the plain PyTorch path with identical semantics.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -17,6 +19,8 @@ from . import kernels as K
 
 
 def _fusable(x: torch.Tensor, weight) -> bool:
+    if os.environ.get("MIVOD_FUSED_BN", "1") == "0":     # eager reference path (tests)
+        return False
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.size(1) % 8 == 0
             and x.is_contiguous(memory_format=torch.channels_last)
             and (weight is None or weight.dtype == torch.float32))
@@ -28,15 +32,60 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous(memory_format=torch.channels_last)
 
 
+class GradSlot:
+    """Side channel for a second gradient stream of a fused op's output.
+
+    A residual network uses a block's input twice (main branch + shortcut);
+    autograd would sum the two gradients with a separate elementwise kernel
+    (3 HBM passes of the activation).  Instead the shortcut use goes through
+    ``tap(x)``, whose backward parks its gradient here and returns None, and
+    the op that PRODUCED x reads it as ``dy2`` inside its own backward kernel
+    (1 extra read).  Autograd still orders the producer after the tap: a None
+    gradient satisfies the dependency edge.
+    """
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
+class _Tap(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, slot):
+        ctx.slot = slot
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g.dim() == 4:
+            g = g.contiguous(memory_format=torch.channels_last)
+        ctx.slot.grad = g if ctx.slot.grad is None else ctx.slot.grad + g
+        return None, None
+
+
+def tap(x: torch.Tensor) -> torch.Tensor:
+    """Second use of a fused op's output whose gradient the producer adds itself."""
+    slot = getattr(x, "_mv_slot", None)
+    if slot is None or not (torch.is_grad_enabled() and x.requires_grad):
+        return x
+    return _Tap.apply(x, slot)
+
+
 class _BNActTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual,
+                slot):
         nat = K.native()
         y, vec = nat.bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, relu,
                                   residual)
         mode = 2 if (relu and residual is not None) else (1 if relu else 0)
         ctx.mode = mode
         ctx.has_res = residual is not None
+        ctx.slot = slot
         ctx.save_for_backward(x, y if mode == 2 else None, vec, weight)
         return y
 
@@ -45,14 +94,17 @@ class _BNActTrain(torch.autograd.Function):
         x, y, vec, weight = ctx.saved_tensors
         dy = _cl(dy)
         need_affine = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
-        dx, dg, db, dz = K.native().bn_bwd(ctx.mode, dy, x, y, vec, weight, need_affine)
+        dy2 = ctx.slot.take() if ctx.slot is not None else None
+        if dy2 is not None and ctx.mode != 2:
+            dy, dy2 = dy + dy2, None
+        dx, dg, db, dz = K.native().bn_bwd(ctx.mode, dy, x, y, vec, weight, need_affine, dy2)
         dres = None
         if ctx.has_res and ctx.needs_input_grad[8]:
             dres = dz if ctx.mode == 2 else dy
         return (dx if ctx.needs_input_grad[0] else None,
                 dg if ctx.needs_input_grad[1] else None,
                 db if ctx.needs_input_grad[2] else None,
-                None, None, None, None, None, dres)
+                None, None, None, None, None, dres, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentum, eps,
@@ -63,8 +115,12 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentu
         if residual is not None:
             residual = _cl(residual)
         if training:
-            return _BNActTrain.apply(x, weight, bias, running_mean, running_var, float(momentum),
-                                     float(eps), bool(relu), residual)
+            slot = GradSlot() if (relu and residual is not None) else None
+            y = _BNActTrain.apply(x, weight, bias, running_mean, running_var, float(momentum),
+                                  float(eps), bool(relu), residual, slot)
+            if slot is not None:
+                y._mv_slot = slot
+            return y
         if not (torch.is_grad_enabled() and (x.requires_grad or (weight is not None and
                                                                  weight.requires_grad))):
             inv = torch.rsqrt(running_var.float() + eps)
@@ -110,3 +166,80 @@ class BatchNorm2d(nn.BatchNorm2d):
     def _load_from_state_dict(self, *args, **kwargs):
         self._mv_steps = 0
         super()._load_from_state_dict(*args, **kwargs)
+
+
+# ------------------------------------------------------------------ pooling
+class _BNReluMaxPool(torch.autograd.Function):
+    """maxpool(relu(bn(x))) for the ResNet stem: statistics pass, then ONE
+    kernel applies BN + ReLU and pools (the full-resolution BN output is never
+    written); backward: gather-form maxpool backward, then BN+ReLU backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, slot):
+        nat = K.native()
+        vec = nat.bn_stats(x, weight, bias, running_mean, running_var, momentum, eps)
+        y, idx = nat.maxpool_fwd(x, vec[2], vec[3], True, k, s, p)
+        ctx.save_for_backward(x, vec, weight, idx)
+        ctx.win, ctx.slot = (k, s, p), slot
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, vec, weight, idx = ctx.saved_tensors
+        nat = K.native()
+        k, s, p = ctx.win
+        dmid = nat.maxpool_bwd(_cl(dy), ctx.slot.take(), idx, x.shape[2], x.shape[3], k, s, p)
+        need_affine = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dx, dg, db, _ = nat.bn_bwd(1, dmid, x, None, vec, weight, need_affine, None)
+        return (dx if ctx.needs_input_grad[0] else None,
+                dg if ctx.needs_input_grad[1] else None,
+                db if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None, None, None, None)
+
+
+def _pool_args(pool: nn.MaxPool2d):
+    def one(v):
+        if isinstance(v, (tuple, list)):
+            if len(set(v)) != 1:
+                return None
+            v = v[0]
+        return int(v)
+    k, s, p = one(pool.kernel_size), one(pool.stride or pool.kernel_size), one(pool.padding)
+    ok = (None not in (k, s, p) and one(pool.dilation) == 1 and not pool.ceil_mode
+          and not pool.return_indices)
+    return (k, s, p) if ok else None
+
+
+def bn_relu_maxpool(x: torch.Tensor, bn: "BatchNorm2d", pool: nn.MaxPool2d) -> torch.Tensor:
+    """``pool(relu(bn(x)))``; fused on GPU in training mode."""
+    win = _pool_args(pool)
+    if (bn.training and bn.track_running_stats and win is not None and
+            _fusable(x, bn.weight) and bn.weight is not None):
+        bn._mv_steps += 1
+        momentum = bn.momentum
+        if momentum is None:
+            momentum = 1.0 / float(bn._mv_steps + int(bn.num_batches_tracked.item()))
+        slot = GradSlot()
+        y = _BNReluMaxPool.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                 float(momentum), float(bn.eps), *win, slot)
+        y._mv_slot = slot
+        return y
+    return pool(bn(x, relu=True))
+
+
+class _GlobalAvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[2], x.shape[3])
+        return K.native().gap_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K.native().gap_bwd(dy.to(torch.bfloat16).contiguous(), *ctx.hw)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """``flatten(adaptive_avg_pool2d(x, 1), 1)`` -> [N, C]."""
+    if _fusable(x, None):
+        return _GlobalAvgPool.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

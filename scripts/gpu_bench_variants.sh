@@ -2,11 +2,8 @@
 # Bench variants in one GPU session (MIOpen cache shared across steps).
 set -u
 mkdir -p gpurun_out
-export MIOPEN_USER_DB_PATH=$PWD/gpurun_out/miopen_db
-export MIOPEN_CUSTOM_CACHE_DIR=$PWD/gpurun_out/miopen_cache
-mkdir -p "$MIOPEN_USER_DB_PATH" "$MIOPEN_CUSTOM_CACHE_DIR"
-[ -d .miopen/db ] && cp -rn .miopen/db/. "$MIOPEN_USER_DB_PATH"/ 2>/dev/null
-[ -d .miopen/cache ] && cp -rn .miopen/cache/. "$MIOPEN_CUSTOM_CACHE_DIR"/ 2>/dev/null
+# bench.py installs the shipped MIOpen find-db / kernel cache (.miopen/) itself,
+# exactly as on the driver's fresh box (scripts/miopen_db_refresh.sh rebuilds it)
 run() {  # run <name> <timeout> <cmd...>
   local name=$1 t=$2; shift 2
   echo "=== $name: $*"

@@ -55,3 +55,9 @@ def test_dropout_keep_mask_rate_and_determinism():
     k3 = dropout_keep_mask(256, 1024, 0.1, 100)
     assert torch.equal(k1, k2) and not torch.equal(k1, k3)
     assert abs((1 - k1.float().mean().item()) - 0.1) < 0.01
+
+
+def test_resnet_zero_init_residual_survives_generic_init():
+    m = resnet50(zero_init_residual=True)
+    assert all(float(b.bn3.weight.abs().sum()) == 0.0 for b in m.modules() if hasattr(b, "bn3"))
+    assert float(m.bn1.weight.sum()) == 64.0
