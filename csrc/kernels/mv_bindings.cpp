@@ -650,6 +650,19 @@ at::Tensor gap_bwd(at::Tensor dy, int64_t H, int64_t W) {
   return dx;
 }
 
+at::Tensor pad_channels(at::Tensor x, int64_t cout) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+              x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "pad_channels: x must be a channels_last bf16 GPU tensor");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C >= 1 && C <= 8 && cout >= C && cout <= 8, "pad_channels: need C <= cout <= 8");
+  c10::DeviceGuard guard(x.device());
+  at::Tensor y = at::empty({N, cout, H, W},
+                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  mv_pad_channels(x.data_ptr(), y.data_ptr(), N * H * W, (int)C, (int)cout, cur_stream());
+  return y;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -684,4 +697,5 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC maxpool backward (gather, + second grad stream)");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pool -> [N, C]");
   m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
+  m.def("pad_channels", &pad_channels, "NHWC zero channel padding C -> cout (<= 8)");
 }

@@ -11,3 +11,4 @@ void mv_maxpool_bwd(const void* dy, const void* dy2, const uint8_t* idx, void* d
                     int W, int C, int OH, int OW, int k, int s, int p, hipStream_t st);
 void mv_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st);
 void mv_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st);
+void mv_pad_channels(const void* x, void* y, int64_t pixels, int cin, int cout, hipStream_t st);

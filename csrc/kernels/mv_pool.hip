@@ -172,6 +172,29 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const __bf16* __restrict__
   store8(dx + t * 8, v);
 }
 
+// Zero-pad the channel dim of an NHWC bf16 tensor, Cin -> Cout (<= 8): the
+// ResNet stem's 3-channel image becomes 4 channels, for which MIOpen's 7x7/2
+// conv kernels run ~1.4x faster (fwd+wgrad); the zero channel changes nothing.
+// One lane per pixel: Cin scalar loads (consecutive lanes read consecutive
+// 2*Cin-byte runs) and one 8-byte store when Cout == 4.
+__global__ __launch_bounds__(256) void pad_channels_kernel(const uint16_t* __restrict__ x,
+                                                           uint16_t* __restrict__ y,
+                                                           int64_t pixels, int cin, int cout) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= pixels) return;
+  uint16_t v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (j < cin) ? x[t * cin + j] : (uint16_t)0;
+  if (cout == 4) {
+    uint2 o;
+    o.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+    o.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
+    *reinterpret_cast<uint2*>(y + t * 4) = o;
+  } else {
+    for (int j = 0; j < cout; ++j) y[t * cout + j] = v[j];
+  }
+}
+
 }  // namespace pool
 }  // namespace mv
 
@@ -210,4 +233,10 @@ void mv_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st) 
   if (!total) return;
   hipLaunchKernelGGL(gap_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
                      (const __bf16*)dy, (__bf16*)dx, N, HW, C);
+}
+
+void mv_pad_channels(const void* x, void* y, int64_t pixels, int cin, int cout, hipStream_t st) {
+  if (!pixels) return;
+  hipLaunchKernelGGL(pad_channels_kernel, dim3(blocks_for(pixels)), dim3(256), 0, st,
+                     (const uint16_t*)x, (uint16_t*)y, pixels, cin, cout);
 }

@@ -12,16 +12,40 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ..ops.bn import BatchNorm2d, bn_relu_maxpool, global_avg_pool, tap
+import os
+
+import torch.nn.functional as F
+
+from ..ops.conv import Conv2d
+from ..ops.bn import BatchNorm2d, bn_relu_maxpool, global_avg_pool, pad_channels, tap
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
-    return nn.Conv2d(cin, cout, 3, stride=stride, padding=dilation, groups=groups, bias=False,
-                     dilation=dilation)
+    return Conv2d(cin, cout, 3, stride=stride, padding=dilation, groups=groups, bias=False,
+                  dilation=dilation)
 
 
 def conv1x1(cin, cout, stride=1):
-    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+    return Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+class StemConv(nn.Conv2d):
+    """The 7x7/2 stem conv.  Parameters stay [64, 3, 7, 7]; on the GPU path the
+    3-channel NHWC image and the weight are zero-padded to 4 channels first
+    (``MIVOD_STEM_CHANNELS``, default 4): MIOpen's gfx950 kernels for Cin=3 run
+    the stem at ~170 TFLOP/s and need an extra 170 us zero-fill, Cin=4 is ~1.4x
+    faster fwd+wgrad (scripts/micro_stem.py).  The zero channel contributes
+    nothing, and its weight gradient is sliced away, so the math is unchanged."""
+
+    def forward(self, x):
+        cp = int(os.environ.get("MIVOD_STEM_CHANNELS", "4"))
+        if (cp > x.shape[1] and x.is_cuda and x.dtype == torch.bfloat16
+                and x.is_contiguous(memory_format=torch.channels_last)):
+            c = x.shape[1]
+            w = F.pad(self.weight, (0, 0, 0, 0, 0, cp - c)).contiguous(
+                memory_format=torch.channels_last)
+            return F.conv2d(pad_channels(x, cp), w, None, self.stride, self.padding)
+        return super().forward(x)
 
 
 class Bottleneck(nn.Module):
@@ -52,7 +76,7 @@ class ResNet(nn.Module):
     def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, zero_init_residual=False):
         super().__init__()
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.conv1 = StemConv(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = BatchNorm2d(64)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(64, layers[0], 1, zero_init_residual)

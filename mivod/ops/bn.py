@@ -243,3 +243,27 @@ def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     if _fusable(x, None):
         return _GlobalAvgPool.apply(x)
     return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+
+
+class _PadChannels(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cout):
+        ctx.c = x.shape[1]
+        return K.native().pad_channels(x, cout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy[:, :ctx.c].contiguous(memory_format=torch.channels_last), None
+
+
+def pad_channels(x: torch.Tensor, cout: int) -> torch.Tensor:
+    """Zero-pad NHWC channels ``C -> cout`` (bf16 channels_last GPU tensors via the
+    ``mv_pool.hip`` kernel; anything else via ``F.pad``)."""
+    if x.shape[1] == cout:
+        return x
+    if (os.environ.get("MIVOD_FUSED_BN", "1") != "0" and x.is_cuda and x.dtype == torch.bfloat16
+            and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)):
+        return _PadChannels.apply(x, cout)
+    return F.pad(x, (0, 0, 0, 0, 0, cout - x.shape[1])).contiguous(
+        memory_format=torch.channels_last if x.is_contiguous(memory_format=torch.channels_last)
+        else torch.contiguous_format)

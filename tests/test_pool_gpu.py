@@ -102,3 +102,56 @@ def test_resnet50_step_fused_no_worse_than_eager_bf16(cuda, monkeypatch):
     err_e = (ge - g32).norm().item() / g32.norm().item()
     assert abs(lf - l32) <= 1.5 * abs(le - l32) + 2e-2, (lf, le, l32)
     assert err_f <= 1.25 * err_e + 1e-2, (err_f, err_e)
+
+
+@pytest.mark.parametrize("shape,cout", [((3, 3, 17, 11), 4), ((2, 3, 224, 224), 4), ((2, 5, 7, 9), 8)])
+def test_pad_channels_kernel(cuda, shape, cout):
+    x = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16))
+    y = K.native().pad_channels(x, cout)
+    assert y.shape == (shape[0], cout, shape[2], shape[3])
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(y[:, :shape[1]], x)
+    assert not y[:, shape[1]:].any()
+
+
+def test_padded_stem_conv_matches_fp32_reference(cuda, monkeypatch):
+    """StemConv (4-channel padded image + weight) vs an fp32 conv of the 3-channel
+    problem: same output, same weight gradient."""
+    from mivod.models.resnet import StemConv
+    torch.manual_seed(0)
+    m = StemConv(3, 64, 7, stride=2, padding=3, bias=False).to(cuda).to(torch.bfloat16)
+    m = m.to(memory_format=torch.channels_last)
+    x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
+    y = m(x)
+    dy = _cl(torch.randn(y.shape, device=cuda).to(torch.bfloat16))
+    y.backward(dy)
+    assert m.weight.grad.shape == (64, 3, 7, 7)
+    w32 = m.weight.detach().float().requires_grad_()
+    y32 = F.conv2d(x.float(), w32, None, 2, 3)
+    y32.backward(dy.float())
+    assert torch.allclose(y.float(), y32, atol=3e-2, rtol=2e-2)
+    rel = (m.weight.grad.float() - w32.grad).norm() / w32.grad.norm()
+    assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("cin,cout,k,hw", [(64, 64, 3, 14), (32, 128, 1, 9), (128, 48, 1, 7),
+                                           (24, 40, 3, 11)])
+def test_conv_dgrad_as_forward_matches_fp32(cuda, cin, cout, k, hw):
+    """mivod.ops.conv.Conv2d: dX computed as a forward conv with the transposed,
+    rotated filter; dW from the backward-weights solver; vs an fp32 reference."""
+    from mivod.ops.conv import Conv2d
+    torch.manual_seed(0)
+    m = Conv2d(cin, cout, k, padding=k // 2, bias=False).to(cuda).to(torch.bfloat16)
+    m = m.to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(3, cin, hw, hw, device=cuda).to(torch.bfloat16)).requires_grad_()
+    y = m(x)
+    assert y.grad_fn is not None and "ConvDgradFwd" in type(y.grad_fn).__name__
+    dy = _cl(torch.randn(y.shape, device=cuda).to(torch.bfloat16))
+    y.backward(dy)
+    x32 = x.detach().float().requires_grad_()
+    w32 = m.weight.detach().float().requires_grad_()
+    y32 = F.conv2d(x32, w32, None, 1, k // 2)
+    y32.backward(dy.float())
+    for got, ref in ((y, y32), (x.grad, x32.grad), (m.weight.grad, w32.grad)):
+        rel = (got.float() - ref).norm() / ref.norm()
+        assert rel < 1e-2, rel
