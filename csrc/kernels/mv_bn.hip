@@ -19,6 +19,9 @@
 #include "mv_common.h"
 #include "mv_bn.h"
 
+#include <mutex>
+#include <unordered_map>
+
 namespace mv {
 namespace bn {
 
@@ -419,42 +422,81 @@ static dim3 grid_of(const Geo& g) {
   return dim3((unsigned)gx, (unsigned)gy);
 }
 
+// ---------------------------------------------------------------- launch shape
+// Every BN pass is one round of exactly the workgroups the chip holds at once
+// (occupancy x CUs, from the HIP occupancy API): with a fixed 2048/4096-block
+// grid the kernels whose VGPR count allows 7 (not 8) workgroups per CU ran a
+// second, 1/7-full round as a tail — the stats pass sat at ~4.6 TB/s
+// (scripts/micro_bn.py).  Each workgroup streams one contiguous row range.
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+static int resident_blocks(const void* fn) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(fn);
+  if (it != cache.end()) return it->second;
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kBlock, 0) != hipSuccess || per < 1)
+    per = 1;
+  const int r = per * num_cus();
+  cache.emplace(fn, r);
+  return r;
+}
+
+// one resident round of workgroups, >= min_rows rows each, <= cap row blocks
+static Geo round_geo(int64_t M, int C, const void* fn, int64_t min_rows, int64_t cap) {
+  Geo g0 = make_geo(M, C, min_rows);
+  const int gy = (C + g0.CB - 1) / g0.CB;
+  int64_t bx = resident_blocks(fn) / gy;
+  if (bx < 1) bx = 1;
+  const int64_t by_rows = (M + min_rows - 1) / min_rows;
+  if (bx > by_rows) bx = by_rows;
+  if (bx > cap) bx = cap;
+  if (bx < 1) bx = 1;
+  return make_geo(M, C, (M + bx - 1) / bx);
+}
+
 }  // namespace bn
 }  // namespace mv
 
 using namespace mv;
 using namespace mv::bn;
 
-// Rows per workgroup for the reduction passes: >= 128 rows and <= 2048 row
-// blocks in total, which keeps the [P][2][C] partials a few % of the input.
+// Upper bound on the row-partials a reduction pass produces (sizes the
+// [P][2][C] workspace); the launchers pick the actual count <= this.
 int mv_bn_partials(int64_t M, int C) {
-  Geo g = make_geo(M, C, 128);
+  Geo g = make_geo(M, C, 64);
   const int gy = (C + g.CB - 1) / g.CB;
-  int64_t p = (M + 127) / 128;
+  int64_t p = (M + 63) / 64;
   const int64_t cap = 2048 / gy > 0 ? 2048 / gy : 1;
   if (p > cap) p = cap;
   if (p < 1) p = 1;
   return (int)p;
 }
 
-static Geo reduce_geo(int64_t M, int C, int P) {
-  return make_geo(M, C, (M + P - 1) / P);
+static Geo reduce_geo(int64_t M, int C, int P, const void* fn) {
+  return round_geo(M, C, fn, 64, P);
 }
 
-static Geo apply_geo(int64_t M, int C) {
-  Geo g0 = make_geo(M, C, 64);
-  const int gy = (C + g0.CB - 1) / g0.CB;
-  int64_t blocks = (M + 63) / 64;
-  const int64_t cap = 4096 / gy > 0 ? 4096 / gy : 1;
-  if (blocks > cap) blocks = cap;
-  return make_geo(M, C, (M + blocks - 1) / blocks);
+static Geo apply_geo(int64_t M, int C, const void* fn) {
+  return round_geo(M, C, fn, 64, 1 << 30);
 }
 
 void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, float* rmean,
                      float* rvar, const float* gamma, const float* beta, float momentum, float eps,
                      bool relu, float* partial, int P, float* save_mean, float* save_invstd,
                      float* scale, float* bias, hipStream_t st) {
-  Geo gr = reduce_geo(M, C, P);
+  Geo gr = reduce_geo(M, C, P, (const void*)&stats_kernel);
   dim3 grr = grid_of(gr);
   hipLaunchKernelGGL(stats_kernel, grr, dim3(kBlock), 0, st, (const __bf16*)x, rmean, partial, gr);
   hipLaunchKernelGGL(finalize_fwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
@@ -463,20 +505,47 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
   if (y) mv_bn_apply(x, res, y, M, C, scale, bias, relu, st);   // y == null: statistics only
 }
 
+template <bool RELU, bool RES>
+static void launch_apply(const __bf16* x, const __bf16* r, const float* scale, const float* bias,
+                         __bf16* y, int64_t M, int C, hipStream_t st) {
+  Geo ga = apply_geo(M, C, (const void*)&apply_kernel<RELU, RES>);
+  hipLaunchKernelGGL((apply_kernel<RELU, RES>), grid_of(ga), dim3(kBlock), 0, st, x, r, scale,
+                     bias, y, ga);
+}
+
 void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
                  const float* bias, bool relu, hipStream_t st) {
-  Geo ga = apply_geo(M, C);
-  dim3 gg = grid_of(ga);
   const __bf16* xp = (const __bf16*)x;
   const __bf16* rp = (const __bf16*)res;
   __bf16* yp = (__bf16*)y;
   if (res) {
-    if (relu) hipLaunchKernelGGL((apply_kernel<true, true>), gg, dim3(kBlock), 0, st, xp, rp, scale, bias, yp, ga);
-    else hipLaunchKernelGGL((apply_kernel<false, true>), gg, dim3(kBlock), 0, st, xp, rp, scale, bias, yp, ga);
+    if (relu) launch_apply<true, true>(xp, rp, scale, bias, yp, M, C, st);
+    else launch_apply<false, true>(xp, rp, scale, bias, yp, M, C, st);
   } else {
-    if (relu) hipLaunchKernelGGL((apply_kernel<true, false>), gg, dim3(kBlock), 0, st, xp, rp, scale, bias, yp, ga);
-    else hipLaunchKernelGGL((apply_kernel<false, false>), gg, dim3(kBlock), 0, st, xp, rp, scale, bias, yp, ga);
+    if (relu) launch_apply<true, false>(xp, rp, scale, bias, yp, M, C, st);
+    else launch_apply<false, false>(xp, rp, scale, bias, yp, M, C, st);
   }
+}
+
+template <int MODE>
+static int launch_bwd_reduce(const __bf16* dy, const __bf16* dy2, const __bf16* x,
+                             const __bf16* y, const float* mean, const float* scale,
+                             const float* bias, __bf16* dz, float* partial, int P, int64_t M,
+                             int C, hipStream_t st) {
+  Geo gr = reduce_geo(M, C, P, (const void*)&bwd_reduce_kernel<MODE>);
+  dim3 grr = grid_of(gr);
+  hipLaunchKernelGGL((bwd_reduce_kernel<MODE>), grr, dim3(kBlock), 0, st, dy, dy2, x, y, mean,
+                     scale, bias, dz, partial, gr);
+  return (int)grr.x;
+}
+
+template <int MODE>
+static void launch_bwd_dx(const __bf16* d, const __bf16* x, const float* scale, const float* bias,
+                          const float* ca, const float* cb, const float* cc, __bf16* dx, int64_t M,
+                          int C, hipStream_t st) {
+  Geo ga = apply_geo(M, C, (const void*)&bwd_dx_kernel<MODE>);
+  hipLaunchKernelGGL((bwd_dx_kernel<MODE>), grid_of(ga), dim3(kBlock), 0, st, d, x, scale, bias,
+                     ca, cb, cc, dx, ga);
 }
 
 void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const void* y, void* dz, void* dx,
@@ -484,27 +553,23 @@ void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const v
                const float* gamma, const float* scale, const float* bias, float* dgamma,
                float* dbeta, float* partial, int P, float* ca, float* cb, float* cc,
                hipStream_t st) {
-  Geo gr = reduce_geo(M, C, P);
-  dim3 grr = grid_of(gr);
   const __bf16* dyp = (const __bf16*)dy;
   const __bf16* dy2p = (const __bf16*)dy2;
   const __bf16* xp = (const __bf16*)x;
   const __bf16* yp = (const __bf16*)y;
   __bf16* dzp = (__bf16*)dz;
+  int pa;
   switch (mode) {
-    case 0: hipLaunchKernelGGL((bwd_reduce_kernel<0>), grr, dim3(kBlock), 0, st, dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
-    case 1: hipLaunchKernelGGL((bwd_reduce_kernel<1>), grr, dim3(kBlock), 0, st, dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
-    default: hipLaunchKernelGGL((bwd_reduce_kernel<2>), grr, dim3(kBlock), 0, st, dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, gr); break;
+    case 0: pa = launch_bwd_reduce<0>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, st); break;
+    case 1: pa = launch_bwd_reduce<1>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, st); break;
+    default: pa = launch_bwd_reduce<2>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, st); break;
   }
   hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
-                     partial, (int)grr.x, M, C, save_mean, save_invstd, gamma, dgamma, dbeta, ca,
-                     cb, cc);
-  Geo ga = apply_geo(M, C);
-  dim3 gg = grid_of(ga);
+                     partial, pa, M, C, save_mean, save_invstd, gamma, dgamma, dbeta, ca, cb, cc);
   __bf16* dxp = (__bf16*)dx;
   switch (mode) {
-    case 0: hipLaunchKernelGGL((bwd_dx_kernel<0>), gg, dim3(kBlock), 0, st, dyp, xp, scale, bias, ca, cb, cc, dxp, ga); break;
-    case 1: hipLaunchKernelGGL((bwd_dx_kernel<1>), gg, dim3(kBlock), 0, st, dyp, xp, scale, bias, ca, cb, cc, dxp, ga); break;
-    default: hipLaunchKernelGGL((bwd_dx_kernel<0>), gg, dim3(kBlock), 0, st, (const __bf16*)dzp, xp, scale, bias, ca, cb, cc, dxp, ga); break;
+    case 0: launch_bwd_dx<0>(dyp, xp, scale, bias, ca, cb, cc, dxp, M, C, st); break;
+    case 1: launch_bwd_dx<1>(dyp, xp, scale, bias, ca, cb, cc, dxp, M, C, st); break;
+    default: launch_bwd_dx<0>((const __bf16*)dzp, xp, scale, bias, ca, cb, cc, dxp, M, C, st); break;
   }
 }
