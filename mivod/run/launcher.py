@@ -18,7 +18,12 @@ torchrun's ``RANK/WORLD_SIZE/LOCAL_RANK/LOCAL_WORLD_SIZE/MASTER_ADDR/MASTER_PORT
 * output is prefixed per rank (``[1,0]<stdout>:`` mpirun style) when
   ``--tag-output`` is given or size > 1;
 * if any rank exits non-zero, the others are terminated (mpirun semantics) and
-  the launcher exits with that code.
+  the launcher exits with that code;
+* horovodrun extras: ``--check-build`` (what this install provides),
+  ``--config-file`` (horovodrun's YAML: params / autotune / timeline /
+  stall_check / logging sections; command-line flags win), ``--output-filename
+  DIR`` (per-rank ``DIR/rank.N/{stdout,stderr}`` copies), ``--disable-cache``,
+  ``--network-interface IF`` (-> ``NCCL_SOCKET_IFNAME`` / ``GLOO_SOCKET_IFNAME``).
 """
 from __future__ import annotations
 
@@ -145,6 +150,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--master-port", type=int, default=0)
     p.add_argument("--ssh-port", type=int, default=None)
     p.add_argument("--network-interface", default=None)
+    p.add_argument("--check-build", action="store_true",
+                   help="print the frameworks / controllers / tensor ops this install provides")
+    p.add_argument("--config-file", default=None, help="horovodrun YAML config file")
+    p.add_argument("--output-filename", default=None,
+                   help="also write each rank's output to DIR/rank.N/{stdout,stderr}")
+    p.add_argument("--disable-cache", action="store_true",
+                   help="disable the coordinator response cache (HOROVOD_CACHE_CAPACITY=0)")
     p.add_argument("--gloo", action="store_true", help="accepted for horovodrun parity")
     p.add_argument("--mpi", action="store_true", help="accepted; mivod never uses MPI")
     # mpirun flags accepted and ignored
@@ -171,6 +183,77 @@ def tuning_env(args) -> Dict[str, str]:
         if getattr(args, flag.lstrip("-").replace("-", "_")):
             env[var] = "1"
     return env
+
+
+# horovodrun --config-file sections -> (flag attribute, env var, converter)
+_CONFIG_KEYS = {
+    ("params", "fusion_threshold_mb"): ("HOROVOD_FUSION_THRESHOLD", lambda v: str(int(float(v) * 2 ** 20))),
+    ("params", "cycle_time_ms"): ("HOROVOD_CYCLE_TIME", str),
+    ("params", "cache_capacity"): ("HOROVOD_CACHE_CAPACITY", str),
+    ("params", "hierarchical_allreduce"): ("HOROVOD_HIERARCHICAL_ALLREDUCE", lambda v: "1" if v else "0"),
+    ("params", "hierarchical_allgather"): ("HOROVOD_HIERARCHICAL_ALLGATHER", lambda v: "1" if v else "0"),
+    ("autotune", "enabled"): ("HOROVOD_AUTOTUNE", lambda v: "1" if v else "0"),
+    ("autotune", "log_file"): ("HOROVOD_AUTOTUNE_LOG", str),
+    ("timeline", "filename"): ("HOROVOD_TIMELINE", str),
+    ("timeline", "mark_cycles"): ("HOROVOD_TIMELINE_MARK_CYCLES", lambda v: "1" if v else "0"),
+    ("stall_check", "enabled"): ("HOROVOD_STALL_CHECK_DISABLE", lambda v: "0" if v else "1"),
+    ("stall_check", "warning_time_seconds"): ("HOROVOD_STALL_CHECK_TIME_SECONDS", str),
+    ("stall_check", "shutdown_time_seconds"): ("HOROVOD_STALL_SHUTDOWN_TIME_SECONDS", str),
+    ("logging", "level"): ("HOROVOD_LOG_LEVEL", str),
+    ("logging", "hide_timestamp"): ("HOROVOD_LOG_HIDE_TIME", lambda v: "1" if v else "0"),
+    ("mivod", "bucket_mb"): ("MIVOD_BUCKET_MB", str),
+    ("mivod", "first_bucket_mb"): ("MIVOD_FIRST_BUCKET_MB", str),
+}
+
+
+def config_file_env(path: str) -> Dict[str, str]:
+    """Env for a horovodrun ``--config-file`` (YAML, safe loader)."""
+    import yaml
+    with open(path) as f:
+        cfg = yaml.safe_load(f) or {}
+    if not isinstance(cfg, dict):
+        raise ValueError(f"{path}: top level must be a mapping")
+    env = {}
+    for section, body in cfg.items():
+        if not isinstance(body, dict):
+            raise ValueError(f"{path}: section {section!r} must be a mapping")
+        for key, val in body.items():
+            ent = _CONFIG_KEYS.get((section, key))
+            if ent is None:
+                raise ValueError(f"{path}: unknown setting {section}.{key}")
+            env[ent[0]] = ent[1](val)
+    return env
+
+
+def check_build() -> str:
+    """horovodrun --check-build equivalent: what this mivod install provides."""
+    def probe(mod):
+        try:
+            __import__(mod)
+            return True
+        except Exception:
+            return False
+
+    def box(ok):
+        return "[X]" if ok else "[ ]"
+
+    import torch
+    dist = probe("torch.distributed")
+    rccl = dist and torch.distributed.is_nccl_available() and torch.version.hip is not None
+    gloo = dist and torch.distributed.is_gloo_available()
+    lines = ["mivod (Horovod API on MI355X)", "",
+             "Available Frameworks:",
+             f"    {box(True)} PyTorch ({torch.__version__})",
+             f"    {box(probe('mivod.kerasfw'))} Keras (mivod.kerasfw on PyTorch)",
+             f"    {box(False)} TensorFlow", f"    {box(False)} MXNet", "",
+             "Available Controllers:",
+             f"    {box(probe('mivod._mvcore'))} TCP coordinator (mivod._mvcore, C++)",
+             f"    {box(False)} MPI", f"    {box(gloo)} Gloo", "",
+             "Available Tensor Operations:",
+             f"    {box(rccl)} RCCL (xGMI)", f"    {box(False)} NCCL", f"    {box(False)} DDL",
+             f"    {box(False)} CCL", f"    {box(False)} MPI", f"    {box(gloo)} Gloo",
+             f"    {box(probe('mivod._mvk'))} gfx950 HIP kernels (mivod._mvk)"]
+    return "\n".join(lines)
 
 
 def exported_env(exports: Sequence[str]) -> Dict[str, str]:
@@ -225,20 +308,28 @@ def ssh_command(host: str, env: Dict[str, str], command: List[str], cwd: str,
 
 
 class _Pump(threading.Thread):
-    def __init__(self, stream, out, prefix: str):
+    def __init__(self, stream, out, prefix: str, copy_path: Optional[str] = None):
         super().__init__(daemon=True)
-        self.stream, self.out, self.prefix = stream, out, prefix
+        self.stream, self.out, self.prefix, self.copy_path = stream, out, prefix, copy_path
 
     def run(self):
-        for line in iter(self.stream.readline, b""):
-            text = line.decode(errors="replace")
-            self.out.write(self.prefix + text if self.prefix else text)
-            self.out.flush()
+        copy = open(self.copy_path, "w") if self.copy_path else None
+        try:
+            for line in iter(self.stream.readline, b""):
+                text = line.decode(errors="replace")
+                self.out.write(self.prefix + text if self.prefix else text)
+                self.out.flush()
+                if copy:
+                    copy.write(text)
+                    copy.flush()
+        finally:
+            if copy:
+                copy.close()
 
 
 def launch(slots: List[Slot], command: List[str], extra_env: Dict[str, str],
            tag_output: bool = False, master_port: int = 0, ssh_port: Optional[int] = None,
-           verbose: bool = False) -> int:
+           verbose: bool = False, output_dir: Optional[str] = None) -> int:
     size = len(slots)
     first = slots[0].host
     master_addr = "127.0.0.1" if _is_local(first) else first
@@ -266,8 +357,13 @@ def launch(slots: List[Slot], command: List[str], extra_env: Dict[str, str],
         procs.append(p)
         pre_o = f"[{s.rank}]<stdout>:" if tag else ""
         pre_e = f"[{s.rank}]<stderr>:" if tag else ""
-        for st, out, pre in ((p.stdout, sys.stdout, pre_o), (p.stderr, sys.stderr, pre_e)):
-            t = _Pump(st, out, pre)
+        rdir = None
+        if output_dir:
+            rdir = os.path.join(output_dir, f"rank.{s.rank}")
+            os.makedirs(rdir, exist_ok=True)
+        for st, out, pre, nm in ((p.stdout, sys.stdout, pre_o, "stdout"),
+                                 (p.stderr, sys.stderr, pre_e, "stderr")):
+            t = _Pump(st, out, pre, os.path.join(rdir, nm) if rdir else None)
             t.start()
             pumps.append(t)
 
@@ -313,6 +409,9 @@ def launch(slots: List[Slot], command: List[str], extra_env: Dict[str, str],
 
 def main(argv: Optional[List[str]] = None) -> int:
     args = build_parser().parse_args(argv)
+    if args.check_build:
+        print(check_build())
+        return 0
     command = list(args.command)
     if command and command[0] == "--":
         command = command[1:]
@@ -326,10 +425,16 @@ def main(argv: Optional[List[str]] = None) -> int:
         hosts = [("localhost", args.np or 1)]
     np = args.np or sum(n for _, n in hosts)
     slots = assign_slots(hosts, np)
-    env = tuning_env(args)
+    env = config_file_env(args.config_file) if args.config_file else {}
+    env.update(tuning_env(args))                  # command-line flags win over the file
+    if args.disable_cache:
+        env["HOROVOD_CACHE_CAPACITY"] = "0"
+    if args.network_interface:
+        env["NCCL_SOCKET_IFNAME"] = args.network_interface
+        env["GLOO_SOCKET_IFNAME"] = args.network_interface
     env.update(exported_env(args.export))
     return launch(slots, command, env, args.tag_output, args.master_port, args.ssh_port,
-                  args.verbose)
+                  args.verbose, args.output_filename)
 
 
 if __name__ == "__main__":

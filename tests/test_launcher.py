@@ -101,3 +101,42 @@ def test_bucket_plan_orders_by_readiness():
     assert plan[0][1] <= 4 * 2 ** 20            # small first bucket
     assert plan[-1][1] <= 5 * 2 ** 20           # small exposed tail
     assert sum(b for _, b, _ in plan) >= 25557032 * 2 * 0.99
+
+
+def test_config_file_maps_sections_and_flags_win(tmp_path):
+    from mivod.run.launcher import config_file_env, main
+    cfg = tmp_path / "hvd.yaml"
+    cfg.write_text("params:\n  fusion_threshold_mb: 16\n  cycle_time_ms: 3\n"
+                   "  hierarchical_allreduce: true\n"
+                   "timeline:\n  filename: /tmp/t.json\n  mark_cycles: true\n"
+                   "stall_check:\n  enabled: false\n  warning_time_seconds: 30\n"
+                   "logging:\n  level: debug\n")
+    env = config_file_env(str(cfg))
+    assert env["HOROVOD_FUSION_THRESHOLD"] == str(16 * 2 ** 20)
+    assert env["HOROVOD_CYCLE_TIME"] == "3" and env["HOROVOD_HIERARCHICAL_ALLREDUCE"] == "1"
+    assert env["HOROVOD_TIMELINE"] == "/tmp/t.json" and env["HOROVOD_TIMELINE_MARK_CYCLES"] == "1"
+    assert env["HOROVOD_STALL_CHECK_DISABLE"] == "1"
+    assert env["HOROVOD_STALL_CHECK_TIME_SECONDS"] == "30" and env["HOROVOD_LOG_LEVEL"] == "debug"
+    bad = tmp_path / "bad.yaml"
+    bad.write_text("params:\n  no_such_knob: 1\n")
+    with pytest.raises(ValueError):
+        config_file_env(str(bad))
+    # the file feeds the ranks; a command-line flag overrides it
+    prog = tmp_path / "show.py"
+    prog.write_text("import os; print('FT', os.environ['HOROVOD_FUSION_THRESHOLD'], "
+                    "'CT', os.environ['HOROVOD_CYCLE_TIME'], 'CC', os.environ['HOROVOD_CACHE_CAPACITY'])\n")
+    r = subprocess.run([sys.executable, "-m", "mivod.run", "-np", "1", "--config-file", str(cfg),
+                        "--cycle-time-ms", "7", "--disable-cache", "--output-filename",
+                        str(tmp_path / "logs"), sys.executable, str(prog)],
+                       cwd=ROOT, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert f"FT {16 * 2 ** 20} CT 7 CC 0" in r.stdout
+    assert f"FT {16 * 2 ** 20} CT 7 CC 0" in (tmp_path / "logs" / "rank.0" / "stdout").read_text()
+
+
+def test_check_build_lists_backends():
+    r = subprocess.run([sys.executable, "-m", "mivod.run", "--check-build"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "[X] PyTorch" in r.stdout and "Available Tensor Operations:" in r.stdout
+    assert "[ ] MPI" in r.stdout and "[X] Gloo" in r.stdout
