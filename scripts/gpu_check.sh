@@ -20,7 +20,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 rocm-smi --showproductname > gpurun_out/smi.log 2>&1 || true
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -q
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
   step smoke 600 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 step bench1 1200 python bench.py --steps ${BENCH_STEPS:-20} --warmup ${BENCH_WARMUP:-10} ${BENCH_ARGS:-}

@@ -336,6 +336,31 @@ def hierarchical():
     print("OK", r)
 
 
+def horovod_namespace():
+    """An unmodified horovod-style PyTorch script: ``import horovod.torch as hvd``."""
+    import horovod.torch as hvd2
+    hvd2.init()
+    r, n = hvd2.rank(), hvd2.size()
+    torch.manual_seed(r)                       # different init per rank ...
+    m = torch.nn.Linear(5, 3)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1 * n)
+    opt = hvd2.DistributedOptimizer(opt, named_parameters=m.named_parameters())
+    hvd2.broadcast_parameters(m.state_dict(), root_rank=0)   # ... made identical
+    hvd2.broadcast_optimizer_state(opt, root_rank=0)
+    x = torch.randn(8, 5, generator=torch.Generator().manual_seed(10 + r))
+    for _ in range(2):
+        opt.zero_grad()
+        m(x).pow(2).mean().backward()
+        opt.step()
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    allf = hvd2.allgather(flat.unsqueeze(0))
+    assert torch.equal(allf[0], allf[-1])
+    avg = hvd2.allreduce(torch.tensor([float(r)]), name="ns.avg")
+    _close(avg, torch.tensor([(n - 1) / 2]))
+    hvd2.shutdown()
+    print("OK", r)
+
+
 def hvd_rank():
     return int(os.environ.get("RANK", "0"))
 

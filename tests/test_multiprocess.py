@@ -94,3 +94,8 @@ def test_keras_tf2_style_2ranks():
 
 def test_hierarchical_allreduce_2x2():
     run_ranks("hierarchical", 4, local_size=2)
+
+
+def test_horovod_namespace_2ranks():
+    """``import horovod.torch as hvd`` scripts run unchanged on mivod."""
+    run_ranks("horovod_namespace", 2)
