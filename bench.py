@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--compression", default="none", choices=["none", "fp16", "bf16"])
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole step (fwd+bwd+allreduce+fused update) in a HIP graph "
+                         "after the warmup steps and replay it (mivod.torch.make_graphed_step)")
     return ap.parse_args()
 
 
@@ -125,12 +128,21 @@ def main():
         return loss
 
     t_w0 = time.perf_counter()
-    for i in range(args.warmup):
-        loss = step()
-        if rank == 0 and (i < 3 or i == args.warmup - 1):
-            torch.cuda.synchronize()
-            print(f"[bench] warmup step {i} done at {time.perf_counter() - t_w0:.1f}s",
-                  file=sys.stderr, flush=True)
+    if args.graph:
+        if args.optimizer == "torch-sgd":
+            raise SystemExit("--graph needs a mivod fused optimizer (sgd / lars)")
+        step = hvd.make_graphed_step(step, opt, model=model, warmup=max(args.warmup, 1))
+        if rank == 0:
+            print(f"[bench] {max(args.warmup, 1)} eager warmup steps + HIP-graph capture done at "
+                  f"{time.perf_counter() - t_w0:.1f}s", file=sys.stderr, flush=True)
+        step()   # first replay (untimed)
+    else:
+        for i in range(args.warmup):
+            loss = step()
+            if rank == 0 and (i < 3 or i == args.warmup - 1):
+                torch.cuda.synchronize()
+                print(f"[bench] warmup step {i} done at {time.perf_counter() - t_w0:.1f}s",
+                      file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     warm_s = time.perf_counter() - t_w0
 
@@ -180,6 +192,7 @@ def main():
                 "optimizer": f"mivod Fused{args.optimizer.upper()} via DistributedOptimizer",
                 "compression": args.compression,
                 "transport": "rccl" if size > 1 else "local",
+                "hip_graph": bool(args.graph),
             },
         }
         print(json.dumps(rec), flush=True)

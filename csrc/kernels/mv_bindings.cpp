@@ -120,24 +120,35 @@ void* model_ptr(const c10::optional<at::Tensor>& model, const at::Tensor& g, int
   return model->data_ptr();
 }
 
+// optional device hyperparameter block [lr, first, bc1, bc2] (HIP-graph replays)
+const float* dyn_ptr(const c10::optional<at::Tensor>& dyn, const at::Tensor& g) {
+  if (!dyn.has_value()) return nullptr;
+  TORCH_CHECK(dyn->is_cuda() && dyn->scalar_type() == at::kFloat && dyn->is_contiguous() &&
+                  dyn->numel() >= 4 && dyn->device() == g.device(),
+              "dyn must be a contiguous fp32 [4] tensor on the grad's device");
+  return dyn->data_ptr<float>();
+}
+
 void sgd_step(at::Tensor g, at::Tensor w, c10::optional<at::Tensor> mom,
               c10::optional<at::Tensor> model, double lr, double momentum, double dampening,
-              double wd, double gscale, bool nesterov, bool first) {
+              double wd, double gscale, bool nesterov, bool first, c10::optional<at::Tensor> dyn) {
   check_flat(g, "grad");
   check_master(g, w, "master");
   if (mom.has_value()) check_master(g, *mom, "momentum");
   int md;
   void* mp = model_ptr(model, g, &md);
+  const float* dp = dyn_ptr(dyn, g);
   c10::DeviceGuard guard(g.device());
   mv_launch_sgd(g.data_ptr(), dtype_code(g), w.data_ptr<float>(),
                 mom.has_value() ? mom->data_ptr<float>() : nullptr, mp, md, g.numel(), (float)lr,
-                (float)momentum, (float)dampening, (float)wd, (float)gscale, nesterov, first,
+                (float)momentum, (float)dampening, (float)wd, (float)gscale, nesterov, first, dp,
                 cur_stream());
 }
 
 void adam_step(at::Tensor g, at::Tensor w, at::Tensor m, at::Tensor v,
                c10::optional<at::Tensor> model, double lr, double b1, double b2, double eps,
-               double wd, double gscale, int64_t step, bool adamw, bool keras_eps) {
+               double wd, double gscale, int64_t step, bool adamw, bool keras_eps,
+               c10::optional<at::Tensor> dyn) {
   check_flat(g, "grad");
   check_master(g, w, "master");
   check_master(g, m, "exp_avg");
@@ -151,12 +162,12 @@ void adam_step(at::Tensor g, at::Tensor w, at::Tensor m, at::Tensor v,
   mv_launch_adam(g.data_ptr(), dtype_code(g), w.data_ptr<float>(), m.data_ptr<float>(),
                  v.data_ptr<float>(), mp, md, g.numel(), (float)lr, (float)b1, (float)b2,
                  (float)eps, (float)wd, (float)gscale, (float)bc1, (float)bc2, adamw, keras_eps,
-                 cur_stream());
+                 dyn_ptr(dyn, g), cur_stream());
 }
 
 void adadelta_step(at::Tensor g, at::Tensor w, at::Tensor sq, at::Tensor acc,
                    c10::optional<at::Tensor> model, double lr, double rho, double eps, double wd,
-                   double gscale) {
+                   double gscale, c10::optional<at::Tensor> dyn) {
   check_flat(g, "grad");
   check_master(g, w, "master");
   check_master(g, sq, "square_avg");
@@ -166,7 +177,7 @@ void adadelta_step(at::Tensor g, at::Tensor w, at::Tensor sq, at::Tensor acc,
   c10::DeviceGuard guard(g.device());
   mv_launch_adadelta(g.data_ptr(), dtype_code(g), w.data_ptr<float>(), sq.data_ptr<float>(),
                      acc.data_ptr<float>(), mp, md, g.numel(), (float)lr, (float)rho, (float)eps,
-                     (float)wd, (float)gscale, cur_stream());
+                     (float)wd, (float)gscale, dyn_ptr(dyn, g), cur_stream());
 }
 
 ChunkTable make_table(const at::Tensor& begin, const at::Tensor& len, const at::Tensor& seg,
@@ -194,7 +205,8 @@ ChunkTable make_table(const at::Tensor& begin, const at::Tensor& len, const at::
 void lars_step(at::Tensor g, at::Tensor w, at::Tensor mom, c10::optional<at::Tensor> model,
                at::Tensor cbeg, at::Tensor clen, at::Tensor cseg, at::Tensor seg_c0,
                at::Tensor seg_nc, at::Tensor sflag, at::Tensor partial, at::Tensor norms, double lr,
-               double momentum, double wd, double eta, double gscale, double eps, bool first) {
+               double momentum, double wd, double eta, double gscale, double eps, bool first,
+               c10::optional<at::Tensor> dyn) {
   check_flat(g, "grad");
   check_master(g, w, "master");
   check_master(g, mom, "momentum");
@@ -210,7 +222,7 @@ void lars_step(at::Tensor g, at::Tensor w, at::Tensor mom, c10::optional<at::Ten
   mv_launch_lars(g.data_ptr(), dtype_code(g), w.data_ptr<float>(), mom.data_ptr<float>(), mp, md,
                  ct, sflag.data_ptr<int32_t>(), partial.data_ptr<float>(), norms.data_ptr<float>(),
                  (float)lr, (float)momentum, (float)wd, (float)eta, (float)gscale, (float)eps, first,
-                 cur_stream());
+                 dyn_ptr(dyn, g), cur_stream());
 }
 
 void seg_dot3(at::Tensor a, at::Tensor b, at::Tensor cbeg, at::Tensor clen, at::Tensor cseg,

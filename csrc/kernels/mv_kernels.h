@@ -30,17 +30,20 @@ void mv_launch_flat_cast(const void* src, int sd, void* dst, int dd, int64_t n, 
                          int* found_nonfinite, hipStream_t st);
 void mv_launch_sgd(const void* g, int gd, float* w, float* mom, void* model, int md, int64_t n,
                    float lr, float momentum, float dampening, float wd, float gscale, int nesterov,
-                   int first, hipStream_t st);
+                   int first, const float* dyn, hipStream_t st);
+// dyn (nullable): device [lr, first, bc1, bc2] read by the kernel instead of the
+// scalar arguments — HIP-graph replayable hyperparameters (mivod/torch/graphs.py)
 void mv_launch_adam(const void* g, int gd, float* w, float* m, float* v, void* model, int md,
                     int64_t n, float lr, float b1, float b2, float eps, float wd, float gscale,
-                    float bc1, float bc2, int adamw, int keras_eps, hipStream_t st);
+                    float bc1, float bc2, int adamw, int keras_eps, const float* dyn,
+                    hipStream_t st);
 void mv_launch_adadelta(const void* g, int gd, float* w, float* sq, float* acc, void* model, int md,
                         int64_t n, float lr, float rho, float eps, float wd, float gscale,
-                        hipStream_t st);
+                        const float* dyn, hipStream_t st);
 void mv_launch_lars(const void* g, int gd, float* w, float* mom, void* model, int md,
                     const ChunkTable& ct, const int32_t* sflag, float* partial, float* norms,
                     float lr, float momentum, float wd, float eta, float gscale, float eps,
-                    int first, hipStream_t st);
+                    int first, const float* dyn, hipStream_t st);
 void mv_launch_seg_dot3(const void* a, const void* b, int dt, const ChunkTable& ct, float* partial,
                         float* out, hipStream_t st);
 void mv_launch_adasum_combine(void* a, const void* b, int dt, const ChunkTable& ct,

@@ -159,6 +159,11 @@ void mv_launch_flat_cast(const void* src, int sd, void* dst, int dd, int64_t n, 
 namespace mv {
 
 struct SgdHp { float lr, momentum, dampening, wd, gscale; int nesterov, first; };
+// Graph-replayable hyperparameters: when ``dyn`` is non-null the kernel reads the
+// per-step values from device memory instead of its by-value launch arguments,
+// so a captured HIP graph keeps following LR schedules and step counters:
+// dyn = [lr, first (0/1), bias_correction1, bias_correction2] (fp32, 16 bytes),
+// refreshed on the stream before every replay (mivod/torch/graphs.py).
 struct AdamHp { float lr, b1, b2, eps, wd, gscale, bc1, bc2; int adamw, keras_eps; };
 struct AdadeltaHp { float lr, rho, eps, wd, gscale; };
 
@@ -170,7 +175,9 @@ __global__ __launch_bounds__(kBlock) void sgd_flat_kernel(const TG* __restrict__
                                                            float* __restrict__ w,
                                                            float* __restrict__ mom,
                                                            TP* __restrict__ model, int64_t n,
-                                                           SgdHp hp) {
+                                                           SgdHp hp,
+                                                           const float* __restrict__ dyn) {
+  if (dyn) { hp.lr = dyn[0]; hp.first = dyn[1] != 0.f; }
   const int64_t base = (int64_t)blockIdx.x * kChunk;
   for (int64_t i = base + threadIdx.x * kVec; i < base + kChunk; i += kBlock * kVec) {
     if (i + kVec <= n) {
@@ -214,7 +221,9 @@ __global__ __launch_bounds__(kBlock) void adam_flat_kernel(const TG* __restrict_
                                                             float* __restrict__ m,
                                                             float* __restrict__ v,
                                                             TP* __restrict__ model, int64_t n,
-                                                            AdamHp hp) {
+                                                            AdamHp hp,
+                                                            const float* __restrict__ dyn) {
+  if (dyn) { hp.lr = dyn[0]; hp.bc1 = dyn[2]; hp.bc2 = dyn[3]; }
   const int64_t base = (int64_t)blockIdx.x * kChunk;
   const float step = hp.lr / hp.bc1;
   const float rbc2 = 1.f / sqrtf(hp.bc2);
@@ -259,7 +268,9 @@ __global__ __launch_bounds__(kBlock) void adadelta_flat_kernel(const TG* __restr
                                                                 float* __restrict__ sq,
                                                                 float* __restrict__ acc,
                                                                 TP* __restrict__ model, int64_t n,
-                                                                AdadeltaHp hp) {
+                                                                AdadeltaHp hp,
+                                                                const float* __restrict__ dyn) {
+  if (dyn) hp.lr = dyn[0];
   const int64_t base = (int64_t)blockIdx.x * kChunk;
   for (int64_t i = base + threadIdx.x * kVec; i < base + kChunk; i += kBlock * kVec) {
     const int cnt = (i + kVec <= n) ? kVec : (i < n ? (int)(n - i) : 0);
@@ -376,7 +387,9 @@ __global__ __launch_bounds__(kBlock) void lars_flat_kernel(const TG* __restrict_
                                                             const int32_t* __restrict__ cseg,
                                                             const int32_t* __restrict__ sflag,
                                                             const float* __restrict__ norms,
-                                                            LarsHp hp) {
+                                                            LarsHp hp,
+                                                            const float* __restrict__ dyn) {
+  if (dyn) { hp.lr = dyn[0]; hp.first = dyn[1] != 0.f; }
   const int c = blockIdx.x;
   const int64_t beg = cbeg[c];
   const int len = clen[c];
@@ -458,35 +471,36 @@ __global__ __launch_bounds__(kBlock) void adasum_combine_kernel(T* __restrict__ 
 
 void mv_launch_sgd(const void* g, int gd, float* w, float* mom, void* model, int md, int64_t n,
                    float lr, float momentum, float dampening, float wd, float gscale, int nesterov,
-                   int first, hipStream_t st) {
+                   int first, const float* dyn, hipStream_t st) {
   if (n <= 0) return;
   SgdHp hp{lr, momentum, dampening, wd, gscale, nesterov, first};
   DISPATCH_GP(gd, md, hipLaunchKernelGGL((sgd_flat_kernel<TG, TP>), MV_GRID(n), dim3(kBlock), 0,
-                                         st, (const TG*)g, w, mom, (TP*)model, n, hp));
+                                         st, (const TG*)g, w, mom, (TP*)model, n, hp, dyn));
 }
 
 void mv_launch_adam(const void* g, int gd, float* w, float* m, float* v, void* model, int md,
                     int64_t n, float lr, float b1, float b2, float eps, float wd, float gscale,
-                    float bc1, float bc2, int adamw, int keras_eps, hipStream_t st) {
+                    float bc1, float bc2, int adamw, int keras_eps, const float* dyn,
+                    hipStream_t st) {
   if (n <= 0) return;
   AdamHp hp{lr, b1, b2, eps, wd, gscale, bc1, bc2, adamw, keras_eps};
   DISPATCH_GP(gd, md, hipLaunchKernelGGL((adam_flat_kernel<TG, TP>), MV_GRID(n), dim3(kBlock), 0,
-                                         st, (const TG*)g, w, m, v, (TP*)model, n, hp));
+                                         st, (const TG*)g, w, m, v, (TP*)model, n, hp, dyn));
 }
 
 void mv_launch_adadelta(const void* g, int gd, float* w, float* sq, float* acc, void* model,
                         int md, int64_t n, float lr, float rho, float eps, float wd, float gscale,
-                        hipStream_t st) {
+                        const float* dyn, hipStream_t st) {
   if (n <= 0) return;
   AdadeltaHp hp{lr, rho, eps, wd, gscale};
   DISPATCH_GP(gd, md, hipLaunchKernelGGL((adadelta_flat_kernel<TG, TP>), MV_GRID(n), dim3(kBlock),
-                                         0, st, (const TG*)g, w, sq, acc, (TP*)model, n, hp));
+                                         0, st, (const TG*)g, w, sq, acc, (TP*)model, n, hp, dyn));
 }
 
 void mv_launch_lars(const void* g, int gd, float* w, float* mom, void* model, int md,
                     const ChunkTable& ct, const int32_t* sflag, float* partial, float* norms,
                     float lr, float momentum, float wd, float eta, float gscale, float eps,
-                    int first, hipStream_t st) {
+                    int first, const float* dyn, hipStream_t st) {
   if (ct.nchunks <= 0) return;
   // pass 1: per-chunk (|w|^2, |g|^2)
   switch (gd) {
@@ -500,7 +514,7 @@ void mv_launch_lars(const void* g, int gd, float* w, float* mom, void* model, in
   LarsHp hp{lr, momentum, wd, eta, gscale, eps, first};
   DISPATCH_GP(gd, md, hipLaunchKernelGGL((lars_flat_kernel<TG, TP>), dim3(ct.nchunks), dim3(kBlock),
                                          0, st, (const TG*)g, w, mom, (TP*)model, ct.begin, ct.len,
-                                         ct.seg, sflag, norms, hp));
+                                         ct.seg, sflag, norms, hp, dyn));
 }
 
 void mv_launch_seg_dot3(const void* a, const void* b, int dt, const ChunkTable& ct, float* partial,

@@ -70,7 +70,8 @@ class _Tap(torch.autograd.Function):
 def tap(x: torch.Tensor) -> torch.Tensor:
     """Second use of a fused op's output whose gradient the producer adds itself."""
     slot = getattr(x, "_mv_slot", None)
-    if slot is None or not (torch.is_grad_enabled() and x.requires_grad):
+    if slot is None or not (torch.is_grad_enabled() and x.requires_grad) or \
+            os.environ.get("MIVOD_BN_TAP", "1") == "0":
         return x
     return _Tap.apply(x, slot)
 

@@ -117,10 +117,12 @@ def flat_cast(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0,
 # K6 fused optimizers (flat)
 # ---------------------------------------------------------------------------
 def sgd_step(g, w, mom, model, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0,
-             gscale=1.0, nesterov=False, first=False):
+             gscale=1.0, nesterov=False, first=False, dyn=None):
+    """``dyn`` (GPU only): device fp32 [lr, first, bc1, bc2] read by the kernel in
+    place of ``lr`` / ``first`` — the HIP-graph replay path (mivod.torch.graphs)."""
     if _on_gpu(g):
         native().sgd_step(g, w, mom, model, float(lr), float(momentum), float(dampening),
-                          float(weight_decay), float(gscale), bool(nesterov), bool(first))
+                          float(weight_decay), float(gscale), bool(nesterov), bool(first), dyn)
         return
     d = g.float() * gscale + weight_decay * w
     if mom is not None:
@@ -135,11 +137,11 @@ def sgd_step(g, w, mom, model, *, lr, momentum=0.0, dampening=0.0, weight_decay=
 
 
 def adam_step(g, w, m, v, model, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
-              gscale=1.0, step=1, adamw=False, keras_eps=False):
+              gscale=1.0, step=1, adamw=False, keras_eps=False, dyn=None):
     if _on_gpu(g):
         native().adam_step(g, w, m, v, model, float(lr), float(beta1), float(beta2), float(eps),
                            float(weight_decay), float(gscale), int(step), bool(adamw),
-                           bool(keras_eps))
+                           bool(keras_eps), dyn)
         return
     gr = g.float() * gscale
     if not adamw and weight_decay:
@@ -160,10 +162,10 @@ def adam_step(g, w, m, v, model, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight
 
 
 def adadelta_step(g, w, sq, acc, model, *, lr=1.0, rho=0.9, eps=1e-6, weight_decay=0.0,
-                  gscale=1.0):
+                  gscale=1.0, dyn=None):
     if _on_gpu(g):
         native().adadelta_step(g, w, sq, acc, model, float(lr), float(rho), float(eps),
-                               float(weight_decay), float(gscale))
+                               float(weight_decay), float(gscale), dyn)
         return
     gr = g.float() * gscale + weight_decay * w
     sq.mul_(rho).addcmul_(gr, gr, value=1 - rho)
@@ -229,7 +231,7 @@ def make_chunk_table(seg_sizes: Sequence[int], device, seg_offsets: Optional[Seq
 
 def lars_step(g, w, mom, model, table: ChunkTable, seg_flags: torch.Tensor, *, lr, momentum=0.9,
               weight_decay=0.0, eta=0.001, gscale=1.0, eps=0.0, first=False,
-              workspace: Optional[dict] = None):
+              workspace: Optional[dict] = None, dyn=None):
     """Segmented LARS (You et al. 2017): per segment trust = eta*|w|/(|g|+wd*|w|);
     flagged segments (bit0) get trust 1 and no weight decay."""
     if _on_gpu(g):
@@ -243,7 +245,8 @@ def lars_step(g, w, mom, model, table: ChunkTable, seg_flags: torch.Tensor, *, l
             norms = ws["norms"] = torch.empty(2 * table.nseg, dtype=torch.float32, device=g.device)
         native().lars_step(g, w, mom, model, table.begin, table.len, table.seg, table.seg_c0,
                            table.seg_nc, seg_flags, partial, norms, float(lr), float(momentum),
-                           float(weight_decay), float(eta), float(gscale), float(eps), bool(first))
+                           float(weight_decay), float(eta), float(gscale), float(eps), bool(first),
+                           dyn)
         return
     flags = seg_flags.tolist()
     for i, (off, n) in enumerate(zip(table.seg_offsets, table.seg_sizes)):

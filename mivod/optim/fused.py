@@ -68,6 +68,7 @@ class Arena:
         self.versions = [p._version for p in params]
         self.tables: Dict[tuple, K.ChunkTable] = {}
         self.workspace: Dict[str, torch.Tensor] = {}
+        self.dyn: Optional[torch.Tensor] = None   # [lr, first, bc1, bc2] for graph replays
 
     # -- views ---------------------------------------------------------------
     def slot(self, flat: torch.Tensor, i: int) -> torch.Tensor:
@@ -116,6 +117,7 @@ class FusedOptimizer(torch.optim.Optimizer):
         self._mv_arenas: Optional[List[Arena]] = None
         self._mv_grad_dtype = grad_dtype
         self._mv_external_grads = False   # True when DistributedOptimizer packs grads
+        self._mv_graph = False            # True while a HIP graph captures the step
 
     # ---- layout ----------------------------------------------------------
     def _mv_build(self, grad_dtype_for=None) -> List[Arena]:
@@ -166,6 +168,14 @@ class FusedOptimizer(torch.optim.Optimizer):
     # ---- the fused update of a bucket ------------------------------------
     def _mv_apply(self, a: Arena, i0: int, i1: int, gscale: float = 1.0):
         raise NotImplementedError
+
+    def _mv_dyn(self, a: Arena):
+        """Device hyperparameter block for graph capture (None in eager mode)."""
+        if not self._mv_graph:
+            return None
+        if a.dyn is None:
+            a.dyn = torch.zeros(4, dtype=torch.float32, device=a.device)
+        return a.dyn
 
     def _mv_slices(self, a: Arena, i0: int, i1: int):
         lo, hi = a.range_of(i0, i1)
@@ -251,7 +261,7 @@ class FusedSGD(FusedOptimizer):
         hp = a.group
         K.sgd_step(g, w, st.get("momentum_buffer"), model, lr=hp["lr"], momentum=hp["momentum"],
                    dampening=hp["dampening"], weight_decay=hp["weight_decay"], gscale=gscale,
-                   nesterov=hp["nesterov"], first=(a.step == 1))
+                   nesterov=hp["nesterov"], first=(a.step == 1), dyn=self._mv_dyn(a))
 
 
 class FusedAdam(FusedOptimizer):
@@ -271,7 +281,7 @@ class FusedAdam(FusedOptimizer):
         b1, b2 = hp["betas"]
         K.adam_step(g, w, st["exp_avg"], st["exp_avg_sq"], model, lr=hp["lr"], beta1=b1, beta2=b2,
                     eps=hp["eps"], weight_decay=hp["weight_decay"], gscale=gscale, step=a.step,
-                    adamw=hp["adamw"], keras_eps=hp["keras_eps"])
+                    adamw=hp["adamw"], keras_eps=hp["keras_eps"], dyn=self._mv_dyn(a))
 
 
 class FusedAdamW(FusedAdam):
@@ -293,7 +303,8 @@ class FusedAdadelta(FusedOptimizer):
         g, w, st, model = self._mv_slices(a, i0, i1)
         hp = a.group
         K.adadelta_step(g, w, st["square_avg"], st["acc_delta"], model, lr=hp["lr"], rho=hp["rho"],
-                        eps=hp["eps"], weight_decay=hp["weight_decay"], gscale=gscale)
+                        eps=hp["eps"], weight_decay=hp["weight_decay"], gscale=gscale,
+                        dyn=self._mv_dyn(a))
 
 
 class FusedLARS(FusedOptimizer):
@@ -319,4 +330,5 @@ class FusedLARS(FusedOptimizer):
             flags = self._mv_flags[key] = torch.tensor(fl, dtype=torch.int32, device=a.device)
         K.lars_step(g, w, st["momentum_buffer"], model, a.table(i0, i1), flags, lr=hp["lr"],
                     momentum=hp["momentum"], weight_decay=hp["weight_decay"], eta=hp["eta"],
-                    gscale=gscale, eps=hp["eps"], first=(a.step == 1), workspace=a.workspace)
+                    gscale=gscale, eps=hp["eps"], first=(a.step == 1), workspace=a.workspace,
+                    dyn=self._mv_dyn(a))

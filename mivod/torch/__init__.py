@@ -13,3 +13,4 @@ from .mpi_ops import (Adasum, Average, HorovodInternalError, Sum, allgather, all
                       alltoall_async, broadcast, broadcast_, broadcast_async, broadcast_async_,
                       join, poll, synchronize)
 from .optimizer import DistributedOptimizer
+from .graphs import GraphedStep, make_graphed_step

@@ -232,6 +232,7 @@ class _DistributedOptimizerMixin:
         self._mvd_synchronized = False
         self._mvd_should_sync = True
         self._mvd_stream = st.comm_stream
+        self._mvd_inline = False          # run comm + fused update on the current stream
         self._mvd_done_event = None
         self._mvd_nonfinite = None
         self._mvd_steps = 0
@@ -259,7 +260,7 @@ class _DistributedOptimizerMixin:
                     "to step(). Increase backward_passes_per_step to accumulate gradients locally.")
             b, _ = self._mvd_where[id(p)]
             b.pending -= 1
-            if b.pending == 0:
+            if b.pending == 0 and not self._mvd_inline:
                 self._mvd_launch_ready()
 
     def _mvd_launch_ready(self):
@@ -304,7 +305,11 @@ class _DistributedOptimizerMixin:
                 for p in b.params:
                     p.grad = None            # freed on the compute stream after the pack
         flat = a.grad[b.lo:b.hi]
-        cuda = flat.is_cuda and self._mvd_stream is not None
+        # inline (no comm-stream fork; launched from synchronize(), after backward) while
+        # a single-rank step is captured into a HIP graph: ROCm runs a two-stream graph
+        # DAG ~15 us/kernel slower than one chain (scripts/debug/graph_speed.py), and
+        # with one rank there is no RCCL to overlap
+        cuda = flat.is_cuda and self._mvd_stream is not None and not self._mvd_inline
         if cuda:
             ev = torch.cuda.Event()
             ev.record()
@@ -367,7 +372,8 @@ class _DistributedOptimizerMixin:
                 if not b.launched:
                     b.pending = 0
             self._mvd_launch_ready()
-            if self._mvd_stream is not None and torch.cuda.is_available():
+            if self._mvd_stream is not None and torch.cuda.is_available() and \
+                    not self._mvd_inline:
                 torch.cuda.current_stream().wait_stream(self._mvd_stream)
             if self._mvd_fused:
                 self._mv_end_step()
