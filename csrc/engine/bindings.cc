@@ -3,6 +3,7 @@
 #include <pybind11/stl.h>
 
 #include "controller.h"
+#include "ring.h"
 #include "timeline.h"
 
 namespace py = pybind11;
@@ -51,6 +52,39 @@ PYBIND11_MODULE(_mvcore, m) {
       .def("mark_cycle", &Timeline::mark_cycle, py::call_guard<py::gil_scoped_release>())
       .def("close", &Timeline::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("events_written", &Timeline::events_written);
+
+  // CPU data plane: ring collectives over TCP on raw host pointers (tensor.data_ptr())
+  py::class_<Ring>(m, "Ring")
+      .def(py::init<int, int, double>(), py::arg("rank"), py::arg("size"),
+           py::arg("timeout_s") = 300.0)
+      .def("listen", &Ring::listen, py::call_guard<py::gil_scoped_release>())
+      .def("connect", &Ring::connect, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce",
+           [](Ring& r, uintptr_t ptr, int64_t count, int dtype, bool average) {
+             r.allreduce((void*)ptr, count, dtype, average);
+           },
+           py::arg("ptr"), py::arg("count"), py::arg("dtype"), py::arg("average") = false,
+           py::call_guard<py::gil_scoped_release>())
+      .def("allgatherv",
+           [](Ring& r, uintptr_t in, uintptr_t out, std::vector<int64_t> bytes) {
+             r.allgatherv((const void*)in, (void*)out, bytes);
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("broadcast",
+           [](Ring& r, uintptr_t ptr, int64_t bytes, int root) {
+             r.broadcast((void*)ptr, bytes, root);
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("barrier", &Ring::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("close", &Ring::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &Ring::rank)
+      .def_property_readonly("size", &Ring::size)
+      .def_property_readonly("bytes_sent", &Ring::bytes_sent);
+  m.def("ring_reduce_sum",
+        [](uintptr_t dst, uintptr_t src, int64_t n, int dtype) {
+          ring_reduce_sum((void*)dst, (const void*)src, n, dtype);
+        },
+        "dst += src (host reducer of the CPU ring; fp16 via F16C, bf16 via fp32 RNE)");
 
   py::class_<ControllerConfig>(m, "ControllerConfig")
       .def(py::init<>())

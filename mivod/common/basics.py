@@ -50,6 +50,8 @@ class _State:
         self.local_pg = None     # intra-node group (hierarchical ops)
         self.cross_pg = None     # one rank per node with equal local_rank
         self.comm_stream = None
+        self.rings = None        # native CPU data plane: [main ring, engine ring] (tcp_ring.py)
+        self.init_count = 0
         self.owns_pg = False
         self.engine = None
         self.lock = threading.RLock()
@@ -175,6 +177,9 @@ def init(comm=None, process_sets=None):
                 else dist.new_group(backend="gloo")
             _state.engine_cpu_pg = dist.new_group(backend="gloo")
             _make_hierarchy_groups()
+            from ..parallel.tcp_ring import make_rings
+            _state.init_count += 1
+            _state.rings = make_rings(_state, generation=_state.init_count)
         else:
             _state.backend = "local"
         _state.initialized = True
@@ -220,6 +225,10 @@ def shutdown():
                 torch.cuda.synchronize()
             except Exception:  # pragma: no cover
                 pass
+        if _state.rings:
+            for r in _state.rings:
+                r.close()
+            _state.rings = None
         if _state.owns_pg and dist.is_initialized():
             try:
                 dist.destroy_process_group()

@@ -34,6 +34,16 @@ def _gloo_ok(dtype: torch.dtype) -> bool:
     return dtype not in (torch.bfloat16,)
 
 
+def _ring(t: torch.Tensor, group, engine: bool):
+    """The native TCP ring (csrc/engine/ring.cc) serving CPU tensors of the whole
+    world, or None (GPU tensor, sub-group, MIVOD_CPU_TRANSPORT=gloo)."""
+    st = basics.state()
+    if t.is_cuda or group is not None or not st.rings:
+        return None
+    from .tcp_ring import supported
+    return st.rings[1 if engine else 0] if supported(t) else None
+
+
 def group_for(t: torch.Tensor, engine: bool = False):
     st = basics.state()
     if t.is_cuda:
@@ -61,6 +71,9 @@ def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
         rop = dist.ReduceOp.AVG if op == Average else dist.ReduceOp.SUM
         dist.all_reduce(t, op=rop, group=pg)
         return t
+    ring = _ring(t, group, engine)
+    if ring is not None:
+        return ring.allreduce_(t, average=(op == Average))
     if _gloo_ok(t.dtype):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg)
         if op == Average:
@@ -113,6 +126,9 @@ def allgather(t: torch.Tensor, group=None, engine: bool = False) -> torch.Tensor
     st = basics.state()
     if st.size == 1:
         return t.clone()
+    ring = _ring(t, group, engine)
+    if ring is not None:
+        return ring.allgather(t)
     pg = group or group_for(t, engine)
     n = torch.tensor([t.shape[0] if t.dim() > 0 else 1], dtype=torch.int64,
                      device=t.device if t.is_cuda else "cpu")
@@ -135,6 +151,9 @@ def broadcast_(t: torch.Tensor, root_rank: int, group=None, engine: bool = False
     st = basics.state()
     if st.size == 1:
         return t
+    ring = _ring(t, group, engine)
+    if ring is not None:
+        return ring.broadcast_(t, root_rank)
     pg = group or group_for(t, engine)
     if t.is_cuda or _gloo_ok(t.dtype):
         if t.is_contiguous():

@@ -361,6 +361,55 @@ def horovod_namespace():
     print("OK", r)
 
 
+def ring():
+    """Native TCP ring data plane (csrc/engine/ring.cc) on CPU tensors."""
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    from mivod.common import basics as B
+    st = B.state()
+    assert st.rings is not None and len(st.rings) == 2, "native ring not active"
+    from mivod.parallel import collectives as C
+    for dt in (torch.float32, torch.float64, torch.float16, torch.bfloat16, torch.int32,
+               torch.int64):
+        for cnt in (0, 1, 7, n - 1, 1000, (1 << 20) + 3):
+            g = torch.Generator().manual_seed(cnt)
+            parts = [(torch.randn(cnt, generator=g) * 4).to(dt) for _ in range(n)]
+            t = parts[r].clone()
+            C.allreduce_(t, C.Sum)
+            exp = sum(p.double() for p in parts) if cnt else torch.zeros(0, dtype=torch.float64)
+            tol = {torch.float16: 0.06, torch.bfloat16: 0.3}.get(dt, 1e-4)
+            assert t.dtype == dt and t.shape == (cnt,)
+            if cnt:
+                err = (t.double() - exp).abs().max().item()
+                assert err <= tol * max(1.0, exp.abs().max().item() / 8), (dt, cnt, err)
+            # bitwise identical on every rank
+            chk = C.allgather(t.view(1, -1) if cnt else t.view(1, 0))
+            assert all(torch.equal(chk[0], chk[i]) for i in range(n)), (dt, cnt)
+    a = torch.full((5,), float(r + 1))
+    C.allreduce_(a, C.Average)
+    assert torch.allclose(a, torch.full((5,), (n + 1) / 2))
+    b = torch.tensor([True, False, r == 0])
+    C.allreduce_(b, C.Sum)
+    assert b.tolist() == [True, False, True]
+    for root in range(n):
+        x = torch.arange(3 * (1 << 19) + 5, dtype=torch.float32) * (r + 1)
+        C.broadcast_(x, root)
+        assert torch.equal(x, torch.arange(3 * (1 << 19) + 5, dtype=torch.float32) * (root + 1))
+    y = torch.full((r + 1, 3), float(r), dtype=torch.float16)
+    g = C.allgather(y)
+    assert g.shape == (sum(range(1, n + 1)), 3)
+    o = 0
+    for k in range(n):
+        assert torch.all(g[o:o + k + 1] == k)
+        o += k + 1
+    # engine ring (named async ops) runs on its own sockets
+    h = hvd.allreduce_async(torch.ones(4) * r, name="ring.async", op=hvd.Sum)
+    _close(hvd.synchronize(h), torch.ones(4) * sum(range(n)))
+    assert st.rings[0].ring.bytes_sent > 0 and st.rings[1].ring.bytes_sent > 0
+    hvd.shutdown()
+    print("OK", r)
+
+
 def hvd_rank():
     return int(os.environ.get("RANK", "0"))
 

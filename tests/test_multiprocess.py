@@ -99,3 +99,10 @@ def test_hierarchical_allreduce_2x2():
 def test_horovod_namespace_2ranks():
     """``import horovod.torch as hvd`` scripts run unchanged on mivod."""
     run_ranks("horovod_namespace", 2)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_native_tcp_ring(n):
+    """C++ ring allreduce / broadcast / allgatherv on CPU tensors (all dtypes incl.
+    fp16 via F16C and bf16), bitwise identical across ranks, odd world sizes."""
+    run_ranks("ring", n)

@@ -26,3 +26,22 @@ def test_controller_under_sanitizer(tmp_path, san):
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     r = subprocess.run([exe, "4"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("san", ["thread", "address,undefined"])
+def test_ring_under_sanitizer(tmp_path, san):
+    """CPU ring data plane (csrc/engine/ring.cc): 4 ranks as threads over loopback."""
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    exe = str(tmp_path / "test_ring")
+    srcs = [os.path.join(ENG, f) for f in ("ring.cc", "wire.cc")] + \
+        [os.path.join(ENG, "tests", "test_ring.cpp")]
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={san}",
+                        "-fno-omit-frame-pointer", "-I", ENG, *srcs, "-o", exe, "-lpthread"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1",
+               ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe, "4"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
