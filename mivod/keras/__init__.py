@@ -62,8 +62,9 @@ def DistributedOptimizer(optimizer, name=None, device_dense="", device_sparse=""
 
 def broadcast_variables(variables, root_rank: int = 0):
     """Broadcast a list of tensors (model variables / optimizer variables) in place."""
-    ts = [v.data if isinstance(v, torch.nn.Parameter) else v for v in variables
-          if torch.is_tensor(v)]
+    # Parameters themselves (broadcast_parameters unwraps .data and bumps the
+    # Parameter's own version counter, which a fused optimizer's master copy tracks)
+    ts = [v for v in variables if torch.is_tensor(v)]
     broadcast_parameters(ts, root_rank)
 
 

@@ -34,6 +34,12 @@ def _gloo_ok(dtype: torch.dtype) -> bool:
     return dtype not in (torch.bfloat16,)
 
 
+def _native_gpu(t: torch.Tensor) -> bool:
+    """GPU tensor on an RCCL world (False for MIVOD_TRANSPORT=gloo-gpu: GPU compute,
+    gloo wire — the multi-rank-on-one-GPU test mode, which lacks AVG and bf16)."""
+    return t.is_cuda and basics.state().backend != "gloo"
+
+
 def _ring(t: torch.Tensor, group, engine: bool):
     """The native TCP ring (csrc/engine/ring.cc) serving CPU tensors of the whole
     world, or None (GPU tensor, sub-group, MIVOD_CPU_TRANSPORT=gloo)."""
@@ -67,7 +73,7 @@ def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
             and st.cross_pg is not None and group is None and not engine
             and t.is_cuda == (st.backend == "nccl")):
         return hierarchical_allreduce_(t, op)
-    if t.is_cuda:
+    if t.is_cuda and st.backend != "gloo":
         rop = dist.ReduceOp.AVG if op == Average else dist.ReduceOp.SUM
         dist.all_reduce(t, op=rop, group=pg)
         return t
@@ -138,7 +144,7 @@ def allgather(t: torch.Tensor, group=None, engine: bool = False) -> torch.Tensor
     src = t if t.dim() > 0 else t.reshape(1)
     rest = tuple(src.shape[1:])
     mx = max(sizes)
-    work_dtype = src.dtype if (t.is_cuda or _gloo_ok(src.dtype)) else torch.float32
+    work_dtype = src.dtype if (_native_gpu(t) or _gloo_ok(src.dtype)) else torch.float32
     pad = torch.zeros((mx,) + rest, dtype=work_dtype, device=src.device)
     pad[:src.shape[0]].copy_(src)
     outs = [torch.empty_like(pad) for _ in range(st.size)]
@@ -155,7 +161,7 @@ def broadcast_(t: torch.Tensor, root_rank: int, group=None, engine: bool = False
     if ring is not None:
         return ring.broadcast_(t, root_rank)
     pg = group or group_for(t, engine)
-    if t.is_cuda or _gloo_ok(t.dtype):
+    if _native_gpu(t) or _gloo_ok(t.dtype):
         if t.is_contiguous():
             dist.broadcast(t, src=root_rank, group=pg)
         else:

@@ -73,6 +73,15 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
         tensors.append(p.data if isinstance(p, torch.nn.Parameter) else p)
     with torch.no_grad():
         _fused_broadcast_(tensors, root_rank)
+    if basics.state().size > 1:
+        # the pack/unpack kernels write through raw pointers: bump the version
+        # counters so in-place edits are visible — a fused optimizer re-seeds its
+        # fp32 master copy of bf16 params from the broadcast values
+        # (Arena.sync_master_if_modified) instead of keeping its own rank's init.
+        # Bump the caller's tensor itself: a Parameter's ``.data`` has its own counter.
+        for _name, p in items:
+            if torch.is_tensor(p):
+                torch.autograd.graph.increment_version(p)
     if tensors and tensors[0].is_cuda:
         torch.cuda.current_stream().synchronize()
 

@@ -1,0 +1,13 @@
+"""Multi-rank GPU hook path on ONE MI355X: 2 ranks share cuda:0 with a gloo wire
+(MIVOD_TRANSPORT=gloo-gpu; RCCL refuses two ranks on one device).  Exercises the
+pack kernel, the comm-stream collective and the fused update kernel with a real
+2-rank reduction — the path the 8-GPU RCCL run takes, minus RCCL itself."""
+import pytest
+
+from test_multiprocess import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+def test_gpu_hook_path_two_ranks_one_gpu(cuda):
+    run_ranks("gpu_dist", 2, timeout=180, extra_env={"MIVOD_TRANSPORT": "gloo-gpu"})
