@@ -34,6 +34,12 @@ def _exchange(send: torch.Tensor, recv: torch.Tensor, peer: int, pg) -> None:
     grank = peer
     if pg is not None and pg is not dist.group.WORLD:
         grank = dist.get_global_rank(pg, peer)
+    if send.is_cuda and basics.state().backend == "gloo":
+        # gloo-gpu test transport: gloo point-to-point moves host tensors only
+        s_h, r_h = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
+        _exchange(s_h, r_h, peer, pg)
+        recv.copy_(r_h)
+        return
     ops = [dist.P2POp(dist.isend, send, grank, group=pg),
            dist.P2POp(dist.irecv, recv, grank, group=pg)]
     for w in dist.batch_isend_irecv(ops):

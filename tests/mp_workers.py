@@ -497,6 +497,49 @@ def gpu_dist():
     print("OK", r)
 
 
+def gpu_adasum():
+    """BASELINE config 5 path on GPU with 2 real ranks (gloo-gpu wire): Adasum kernels
+    (seg_dot3 / adasum_combine) vs a float64 reference, then DistributedOptimizer with
+    fp16 wire compression + Adasum + FusedAdamW keeps the ranks bit-identical."""
+    import numpy as np
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    dev = hvd.device()
+    vecs = [np.random.RandomState(7 + rr).randn(1000) for rr in range(n)]
+
+    def comb(a, b):
+        d = a @ b
+        return (1 - d / (2 * (a @ a))) * a + (1 - d / (2 * (b @ b))) * b
+
+    cur = list(vecs)
+    while len(cur) > 1:
+        cur = [comb(cur[i], cur[i + 1]) for i in range(0, len(cur), 2)]
+    out = hvd.allreduce(torch.tensor(vecs[r], dtype=torch.float32, device=dev), op=hvd.Adasum,
+                        name="gada")
+    np.testing.assert_allclose(out.cpu().numpy(), cur[0], rtol=1e-4, atol=1e-4)
+    from mivod.optim import FusedAdamW
+    torch.manual_seed(0)
+    m = _toy(0).to(dev)
+    opt = hvd.DistributedOptimizer(FusedAdamW(m.parameters(), lr=1e-3),
+                                   named_parameters=m.named_parameters(),
+                                   compression=hvd.Compression.fp16, op=hvd.Adasum,
+                                   bucket_mb=0.005, first_bucket_mb=0.001)
+    g = torch.Generator().manual_seed(100 + r)
+    x, y = torch.randn(4, 3, 8, 8, generator=g).to(dev), torch.randint(0, 10, (4,), generator=g).to(dev)
+    before = [p.detach().clone() for p in m.parameters()]
+    for _ in range(3):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    assert any((p.detach() - q).abs().max() > 0 for p, q in zip(m.parameters(), before))
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    allf = hvd.allgather(flat.unsqueeze(0))
+    assert torch.isfinite(allf).all() and torch.equal(allf[0], allf[-1])
+    hvd.shutdown()
+    print("OK", r)
+
+
 def hvd_rank():
     return int(os.environ.get("RANK", "0"))
 

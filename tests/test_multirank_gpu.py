@@ -11,3 +11,8 @@ pytestmark = pytest.mark.gpu
 
 def test_gpu_hook_path_two_ranks_one_gpu(cuda):
     run_ranks("gpu_dist", 2, timeout=180, extra_env={"MIVOD_TRANSPORT": "gloo-gpu"})
+
+
+def test_gpu_adasum_fp16_two_ranks_one_gpu(cuda):
+    """Config-5 path (fp16 wire + Adasum + FusedAdamW) with 2 real ranks on one GPU."""
+    run_ranks("gpu_adasum", 2, timeout=180, extra_env={"MIVOD_TRANSPORT": "gloo-gpu"})
