@@ -140,3 +140,43 @@ def test_check_build_lists_backends():
     assert r.returncode == 0, r.stderr
     assert "[X] PyTorch" in r.stdout and "Available Tensor Operations:" in r.stdout
     assert "[ ] MPI" in r.stdout and "[X] Gloo" in r.stdout
+
+
+FAKE_SSH = r'''#!/bin/bash
+# test double for ssh: record the call, drop options, run the remote command locally.
+# "fakenode" stands in for a remote host name (no DNS here): map it to loopback.
+echo "$@" >> "%(log)s"
+while [[ "$1" == -* ]]; do
+  case "$1" in -o|-p) shift 2 ;; *) shift ;; esac
+done
+host="$1"; shift
+remote="$*"
+exec bash -c "${remote//fakenode/127.0.0.1}"
+'''
+
+
+def test_launch_remote_hosts_over_ssh(tmp_path):
+    """-H with a non-local host goes through ssh: options, port, cwd and the rank env
+    (HOROVOD_*, MASTER_*, -x exports) are carried on the remote command line."""
+    log = tmp_path / "ssh.log"
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    ssh = bindir / "ssh"
+    ssh.write_text(FAKE_SSH % {"log": log})
+    ssh.chmod(0o755)
+    f = tmp_path / "prog.py"
+    f.write_text(SCRIPT)
+    env = dict(os.environ, MIVOD_TRANSPORT="gloo", PYTHONPATH=ROOT,
+               PATH=f"{bindir}{os.pathsep}{os.environ['PATH']}")
+    r = subprocess.run([sys.executable, "-m", "mivod.run", "-np", "2", "-H", "fakenode:2",
+                        "--ssh-port", "2222", "-x", "NCCL_DEBUG=INFO", "-x", "PYTHONPATH",
+                        "-x", "MIVOD_TRANSPORT", sys.executable, str(f)],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "[0]<stdout>:rank 0 size 2 local 0 sum 1.0 nccl_debug INFO" in r.stdout, r.stdout
+    assert "[1]<stdout>:rank 1 size 2 local 1 sum 1.0 nccl_debug INFO" in r.stdout, r.stdout
+    calls = log.read_text().splitlines()
+    assert len(calls) == 2
+    for c in calls:
+        assert "-p 2222" in c and "BatchMode=yes" in c and " fakenode " in c
+        assert f"cd {ROOT}" in c and "HOROVOD_SIZE=2" in c and "MASTER_ADDR=fakenode" in c
