@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--per-step-marker", default="sgd_flat_kernel")
     ap.add_argument("--markers-per-step", type=int, default=5)
+    ap.add_argument("--total-steps", type=int, default=0,
+                    help="steps the profiled run executed in all (infers markers per step)")
     ap.add_argument("--title", default="")
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
@@ -29,6 +31,8 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     marks = [i for i, r in enumerate(rows) if a.per_step_marker in r[2]]
+    if a.total_steps:
+        a.markers_per_step = len(marks) // a.total_steps
     need = a.markers_per_step * (a.steps + 1)
     if len(marks) < need:
         raise SystemExit(f"only {len(marks)} marker launches, need {need}")
