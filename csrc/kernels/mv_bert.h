@@ -36,6 +36,7 @@ struct LnBwdParams {
   float p_drop;
   uint32_t seed;
   uint32_t thresh;
+  const void* dy2;    // [M, H] second gradient of y (tapped residual use), or nullptr
 };
 
 int64_t mv_bias_gelu_partials(int64_t M, int N);

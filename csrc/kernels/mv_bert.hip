@@ -227,6 +227,7 @@ struct LnBwdArgs {
   float p_drop;
   uint32_t seed;
   uint32_t thresh;
+  const __bf16* dy2;    // [M, H] second gradient stream of y, added on load, or null
 };
 
 // Write one wave-partial set (this wave's 8 x NCH columns) into LDS slot w, then
@@ -272,6 +273,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
       if (c < a.H) {
         float dy[8], vv[8], gm[8];
         load8(a.dy + row * a.H + c, dy);
+        if (a.dy2) {   // residual use of y (mivod.ops.bn.tap): no separate autograd add
+          float e[8];
+          load8(a.dy2 + row * a.H + c, e);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dy[j] += e[j];
+        }
         load8(a.v + row * a.H + c, vv);
         load8(a.gamma + c, gm);
 #pragma unroll
@@ -368,7 +375,8 @@ void mv_ln_fwd(const LnFwdParams& p, hipStream_t st) {
 
 void mv_ln_bwd(const LnBwdParams& p, void* dgamma, void* dbeta, void* dbias, hipStream_t st) {
   LnBwdArgs a{(const __bf16*)p.dy, (const __bf16*)p.v, p.mean, p.rstd, (const __bf16*)p.gamma,
-              (__bf16*)p.dv, (__bf16*)p.dz, p.partial, p.M, p.H, p.p_drop, p.seed, p.thresh};
+              (__bf16*)p.dv, (__bf16*)p.dz, p.partial, p.M, p.H, p.p_drop, p.seed, p.thresh,
+              (const __bf16*)p.dy2};
   const int64_t P = mv_ln_partials(p.M);
   const dim3 g((unsigned)P);
   if (p.H <= 512) hipLaunchKernelGGL(ln_bwd_kernel<1>, g, dim3(256), 0, st, a);

@@ -553,11 +553,13 @@ std::vector<at::Tensor> ln_fwd(at::Tensor z, c10::optional<at::Tensor> bias,
 
 // -> {dv, dz (undefined when p_drop == 0: equals dv), dgamma, dbeta, dbias}
 std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor v, at::Tensor mean, at::Tensor rstd,
-                               at::Tensor gamma, double p_drop, int64_t seed, bool need_dbias) {
+                               at::Tensor gamma, double p_drop, int64_t seed, bool need_dbias,
+                               c10::optional<at::Tensor> dy2) {
   c10::DeviceGuard guard(dy.device());
   const int64_t H = gamma.numel(), M = H ? dy.numel() / H : 0;
   TORCH_CHECK(H % 8 == 0 && H <= 4096, "ln: hidden size must be a multiple of 8, <= 4096");
   check_rows(dy, M, H, "dy");
+  if (dy2.has_value()) check_rows(*dy2, M, H, "dy2");
   check_rows(v, M, H, "v");
   check_rows(gamma, 1, H, "gamma");
   TORCH_CHECK(mean.numel() == M && rstd.numel() == M && mean.scalar_type() == at::kFloat &&
@@ -584,6 +586,7 @@ std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor v, at::Tensor mean, at:
     p.p_drop = (float)p_drop;
     p.seed = (uint32_t)seed;
     p.thresh = drop_thresh(p_drop);
+    p.dy2 = dy2.has_value() ? dy2->data_ptr() : nullptr;
     mv_ln_bwd(p, dg.data_ptr(), db.data_ptr(), need_dbias ? dbias.data_ptr() : nullptr,
               cur_stream());
   }

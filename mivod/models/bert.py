@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.bn import tap
 from ..ops.transformer import bias_dropout_add_ln, bias_gelu
 
 
@@ -86,8 +87,9 @@ class BertSelfAttention(nn.Module):
         b, s, hd = x.shape
         qkv = self.qkv(x).view(b, s, 3, self.h, self.d)
         ctx = attention(qkv, mask_bias, self.p_attn if self.training else 0.0)   # [b, s, h*d]
-        # dense GEMM without bias; bias + dropout + residual + LayerNorm fused
-        return bias_dropout_add_ln(F.linear(ctx, self.dense.weight), self.dense.bias, x,
+        # dense GEMM without bias; bias + dropout + residual + LayerNorm fused; the
+        # residual use of x is tapped: its gradient joins x's producer LN backward
+        return bias_dropout_add_ln(F.linear(ctx, self.dense.weight), self.dense.bias, tap(x),
                                    self.LayerNorm, self.dropout.p, self.training)
 
 
@@ -103,7 +105,7 @@ class BertLayer(nn.Module):
     def forward(self, x, mask_bias):
         a = self.attention(x, mask_bias)
         h = bias_gelu(F.linear(a, self.intermediate.weight), self.intermediate.bias)
-        return bias_dropout_add_ln(F.linear(h, self.output.weight), self.output.bias, a,
+        return bias_dropout_add_ln(F.linear(h, self.output.weight), self.output.bias, tap(a),
                                    self.LayerNorm, self.dropout.p, self.training)
 
 

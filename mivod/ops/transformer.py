@@ -61,11 +61,12 @@ def bias_gelu(x: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 class _BiasDropoutAddLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, z, bias, res, gamma, beta, eps, p, seed):
+    def forward(ctx, z, bias, res, gamma, beta, eps, p, seed, slot):
         N = K.native()
         y, v, mean, rstd = N.ln_fwd(z, _bf16c(bias), res, _bf16c(gamma), _bf16c(beta),
                                     float(eps), float(p), int(seed), True)
         ctx.save_for_backward(v, mean, rstd, _bf16c(gamma))
+        ctx.slot = slot
         ctx.p, ctx.seed = float(p), int(seed)
         ctx.has_bias, ctx.has_res = bias is not None, res is not None
         ctx.dtypes = (gamma.dtype, beta.dtype, None if bias is None else bias.dtype)
@@ -74,25 +75,37 @@ class _BiasDropoutAddLN(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         v, mean, rstd, gamma = ctx.saved_tensors
+        # the residual use of y (tap) parked its gradient here: the kernel adds it on load
+        dy2 = ctx.slot.take() if ctx.slot is not None else None
         dv, dz, dg, db, dbias = K.native().ln_bwd(_bf16c(dy), v, mean, rstd, gamma, ctx.p,
-                                                  ctx.seed, ctx.has_bias)
+                                                  ctx.seed, ctx.has_bias, _bf16c(dy2))
         if dz is None:
             dz = dv                      # no dropout: d(z + b) == d(sum)
         gd, bd, bsd = ctx.dtypes
         return (dz, dbias.to(bsd) if ctx.has_bias else None, dv if ctx.has_res else None,
-                dg.to(gd), db.to(bd), None, None, None)
+                dg.to(gd), db.to(bd), None, None, None, None)
 
 
 def bias_dropout_add_ln(z: torch.Tensor, bias, residual, ln: torch.nn.LayerNorm,
                         p: float = 0.0, training: bool = True) -> torch.Tensor:
-    """``ln(residual + dropout(z + bias))``; ``bias`` / ``residual`` may be None."""
+    """``ln(residual + dropout(z + bias))``; ``bias`` / ``residual`` may be None.
+
+    The fused output carries a gradient slot: a second consumer that uses it as a
+    residual should receive ``mivod.ops.bn.tap(y)``, so the LayerNorm backward adds
+    that gradient while loading ``dy`` instead of autograd adding the two streams
+    with a separate kernel (BERT: 48 bf16 adds of [tokens, 1024] per step)."""
     p = float(p) if training else 0.0
     H = z.shape[-1]
     if (_fused_ok(z) and H % 8 == 0 and H <= 4096 and ln.elementwise_affine and
             ln.normalized_shape == (H,)):
         res = None if residual is None else residual.to(torch.bfloat16).contiguous()
-        return _BiasDropoutAddLN.apply(z.contiguous(), bias, res, ln.weight, ln.bias, ln.eps,
-                                       p, _seed(p))
+        from .bn import GradSlot
+        slot = GradSlot() if torch.is_grad_enabled() else None
+        y = _BiasDropoutAddLN.apply(z.contiguous(), bias, res, ln.weight, ln.bias, ln.eps,
+                                    p, _seed(p), slot)
+        if slot is not None:
+            y._mv_slot = slot        # a later residual use goes through ops.bn.tap(y)
+        return y
     t = z if bias is None else z + bias
     if p > 0:
         t = F.dropout(t, p, True)
