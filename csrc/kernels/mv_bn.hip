@@ -19,6 +19,7 @@
 #include "mv_common.h"
 #include "mv_bn.h"
 
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 
@@ -44,6 +45,15 @@ __device__ __forceinline__ void lane_map(const Geo& g, int* tc, int* tr, int* c,
   *tr = threadIdx.x / g.TPR;
   *c = blockIdx.y * g.CB + *tc * kVec;
   *valid = (*tr < g.RPI) && (*c < g.C);
+}
+
+// Last read of a streamed activation (apply / dx passes: the statistics pass already
+// read it): non-temporal, so it does not push reusable lines out of L2 / MALL.
+// MIVOD_BN_NT=0 at run time selects default-policy loads (A/B switch).
+template <bool NT>
+__device__ __forceinline__ void ldlast(const __bf16* p, float (&v)[8]) {
+  if (NT) load8_nt(p, v);
+  else load8(p, v);
 }
 
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
@@ -183,7 +193,7 @@ __global__ __launch_bounds__(kBlock) void finalize_fwd_kernel(
   bias[ch] = (beta ? beta[ch] : 0.f) - mean * sc;
 }
 
-template <bool RELU, bool RES>
+template <bool RELU, bool RES, bool NT = true>
 __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict__ x,
                                                         const __bf16* __restrict__ res,
                                                         const float* __restrict__ scale,
@@ -202,9 +212,9 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict_
   for (; r + g.RPI < r1; r += 2 * g.RPI) {
     float v0[8], v1[8], q0[8], q1[8];
     const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
-    load8(x + o0, v0);
-    load8(x + o1, v1);
-    if (RES) { load8(res + o0, q0); load8(res + o1, q1); }
+    ldlast<NT>(x + o0, v0);
+    ldlast<NT>(x + o1, v1);
+    if (RES) { ldlast<NT>(res + o0, q0); ldlast<NT>(res + o1, q1); }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float a = __builtin_fmaf(v0[j], sc[j], bi[j]);
@@ -220,8 +230,8 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict_
   for (; r < r1; r += g.RPI) {
     float v0[8], q0[8];
     const int64_t o0 = r * g.C + c;
-    load8(x + o0, v0);
-    if (RES) load8(res + o0, q0);
+    ldlast<NT>(x + o0, v0);
+    if (RES) ldlast<NT>(res + o0, q0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float a = __builtin_fmaf(v0[j], sc[j], bi[j]);
@@ -250,7 +260,9 @@ __device__ __forceinline__ void masked(const float (&dy)[8], const float (&x)[8]
   }
 }
 
-template <int MODE>
+// last-use reads (dy2, the saved output y, and dy in MODE 2 where the dx pass reads dz)
+// are non-temporal
+template <int MODE, bool NT = true>
 __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
     const __bf16* __restrict__ dy, const __bf16* __restrict__ dy2, const __bf16* __restrict__ x,
     const __bf16* __restrict__ y,
@@ -271,18 +283,18 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
     for (; r + g.RPI < r1; r += 2 * g.RPI) {
       float a0[8], a1[8], x0[8], x1[8], y0[8], y1[8], d0[8], d1[8];
       const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
-      load8(dy + o0, a0);
-      load8(dy + o1, a1);
+      if (MODE == 2) ldlast<NT>(dy + o0, a0); else load8(dy + o0, a0);
+      if (MODE == 2) ldlast<NT>(dy + o1, a1); else load8(dy + o1, a1);
       if (dy2) {   // second gradient stream of a tapped output (uniform branch)
         float b0[8], b1[8];
-        load8(dy2 + o0, b0);
-        load8(dy2 + o1, b1);
+        ldlast<NT>(dy2 + o0, b0);
+        ldlast<NT>(dy2 + o1, b1);
 #pragma unroll
         for (int j = 0; j < 8; ++j) { a0[j] += b0[j]; a1[j] += b1[j]; }
       }
       load8(x + o0, x0);
       load8(x + o1, x1);
-      if (MODE == 2) { load8(y + o0, y0); load8(y + o1, y1); }
+      if (MODE == 2) { ldlast<NT>(y + o0, y0); ldlast<NT>(y + o1, y1); }
       masked<MODE>(a0, x0, y0, sc, bi, d0);
       masked<MODE>(a1, x1, y1, sc, bi, d1);
       if (MODE == 2) { store8(dz + o0, d0); store8(dz + o1, d1); }
@@ -295,15 +307,15 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
     for (; r < r1; r += g.RPI) {
       float a0[8], x0[8], y0[8], d0[8];
       const int64_t o0 = r * g.C + c;
-      load8(dy + o0, a0);
+      if (MODE == 2) ldlast<NT>(dy + o0, a0); else load8(dy + o0, a0);
       if (dy2) {
         float b0[8];
-        load8(dy2 + o0, b0);
+        ldlast<NT>(dy2 + o0, b0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) a0[j] += b0[j];
       }
       load8(x + o0, x0);
-      if (MODE == 2) load8(y + o0, y0);
+      if (MODE == 2) ldlast<NT>(y + o0, y0);
       masked<MODE>(a0, x0, y0, sc, bi, d0);
       if (MODE == 2) store8(dz + o0, d0);
 #pragma unroll
@@ -350,7 +362,7 @@ __global__ __launch_bounds__(kBlock) void finalize_bwd_kernel(
   cc[ch] = -a * sdz * inv_m - b * mean[ch];
 }
 
-template <int MODE>
+template <int MODE, bool NT = true>
 __global__ __launch_bounds__(kBlock) void bwd_dx_kernel(
     const __bf16* __restrict__ d_in, const __bf16* __restrict__ x,
     const float* __restrict__ scale, const float* __restrict__ bias, const float* __restrict__ ca,
@@ -370,10 +382,10 @@ __global__ __launch_bounds__(kBlock) void bwd_dx_kernel(
   for (; r + g.RPI < r1; r += 2 * g.RPI) {
     float d0[8], d1[8], x0[8], x1[8];
     const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
-    load8(d_in + o0, d0);
-    load8(d_in + o1, d1);
-    load8(x + o0, x0);
-    load8(x + o1, x1);
+    ldlast<NT>(d_in + o0, d0);
+    ldlast<NT>(d_in + o1, d1);
+    ldlast<NT>(x + o0, x0);
+    ldlast<NT>(x + o1, x1);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float e0 = d0[j], e1 = d1[j];
@@ -390,8 +402,8 @@ __global__ __launch_bounds__(kBlock) void bwd_dx_kernel(
   for (; r < r1; r += g.RPI) {
     float d0[8], x0[8];
     const int64_t o0 = r * g.C + c;
-    load8(d_in + o0, d0);
-    load8(x + o0, x0);
+    ldlast<NT>(d_in + o0, d0);
+    ldlast<NT>(x + o0, x0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float e0 = d0[j];
@@ -484,6 +496,15 @@ int mv_bn_partials(int64_t M, int C) {
   return (int)p;
 }
 
+// MIVOD_BN_NT (default 1): non-temporal last-use loads in the apply / dx passes
+static bool bn_nt() {
+  static const bool on = [] {
+    const char* e = std::getenv("MIVOD_BN_NT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static Geo reduce_geo(int64_t M, int C, int P, const void* fn) {
   return round_geo(M, C, fn, 64, P);
 }
@@ -508,9 +529,15 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
 template <bool RELU, bool RES>
 static void launch_apply(const __bf16* x, const __bf16* r, const float* scale, const float* bias,
                          __bf16* y, int64_t M, int C, hipStream_t st) {
-  Geo ga = apply_geo(M, C, (const void*)&apply_kernel<RELU, RES>);
-  hipLaunchKernelGGL((apply_kernel<RELU, RES>), grid_of(ga), dim3(kBlock), 0, st, x, r, scale,
-                     bias, y, ga);
+  if (bn_nt()) {
+    Geo ga = apply_geo(M, C, (const void*)&apply_kernel<RELU, RES, true>);
+    hipLaunchKernelGGL((apply_kernel<RELU, RES, true>), grid_of(ga), dim3(kBlock), 0, st, x, r,
+                       scale, bias, y, ga);
+  } else {
+    Geo ga = apply_geo(M, C, (const void*)&apply_kernel<RELU, RES, false>);
+    hipLaunchKernelGGL((apply_kernel<RELU, RES, false>), grid_of(ga), dim3(kBlock), 0, st, x, r,
+                       scale, bias, y, ga);
+  }
 }
 
 void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
@@ -532,10 +559,17 @@ static int launch_bwd_reduce(const __bf16* dy, const __bf16* dy2, const __bf16* 
                              const __bf16* y, const float* mean, const float* scale,
                              const float* bias, __bf16* dz, float* partial, int P, int64_t M,
                              int C, hipStream_t st) {
-  Geo gr = reduce_geo(M, C, P, (const void*)&bwd_reduce_kernel<MODE>);
+  if (bn_nt()) {
+    Geo gr = reduce_geo(M, C, P, (const void*)&bwd_reduce_kernel<MODE, true>);
+    dim3 grr = grid_of(gr);
+    hipLaunchKernelGGL((bwd_reduce_kernel<MODE, true>), grr, dim3(kBlock), 0, st, dy, dy2, x, y,
+                       mean, scale, bias, dz, partial, gr);
+    return (int)grr.x;
+  }
+  Geo gr = reduce_geo(M, C, P, (const void*)&bwd_reduce_kernel<MODE, false>);
   dim3 grr = grid_of(gr);
-  hipLaunchKernelGGL((bwd_reduce_kernel<MODE>), grr, dim3(kBlock), 0, st, dy, dy2, x, y, mean,
-                     scale, bias, dz, partial, gr);
+  hipLaunchKernelGGL((bwd_reduce_kernel<MODE, false>), grr, dim3(kBlock), 0, st, dy, dy2, x, y,
+                     mean, scale, bias, dz, partial, gr);
   return (int)grr.x;
 }
 
@@ -543,9 +577,15 @@ template <int MODE>
 static void launch_bwd_dx(const __bf16* d, const __bf16* x, const float* scale, const float* bias,
                           const float* ca, const float* cb, const float* cc, __bf16* dx, int64_t M,
                           int C, hipStream_t st) {
-  Geo ga = apply_geo(M, C, (const void*)&bwd_dx_kernel<MODE>);
-  hipLaunchKernelGGL((bwd_dx_kernel<MODE>), grid_of(ga), dim3(kBlock), 0, st, d, x, scale, bias,
-                     ca, cb, cc, dx, ga);
+  if (bn_nt()) {
+    Geo ga = apply_geo(M, C, (const void*)&bwd_dx_kernel<MODE, true>);
+    hipLaunchKernelGGL((bwd_dx_kernel<MODE, true>), grid_of(ga), dim3(kBlock), 0, st, d, x, scale,
+                       bias, ca, cb, cc, dx, ga);
+  } else {
+    Geo ga = apply_geo(M, C, (const void*)&bwd_dx_kernel<MODE, false>);
+    hipLaunchKernelGGL((bwd_dx_kernel<MODE, false>), grid_of(ga), dim3(kBlock), 0, st, d, x,
+                       scale, bias, ca, cb, cc, dx, ga);
+  }
 }
 
 void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const void* y, void* dz, void* dx,

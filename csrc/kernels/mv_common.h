@@ -47,6 +47,12 @@ __device__ __forceinline__ void load8(const __bf16* p, float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = __uint_as_float(((uint32_t)a[j]) << 16);
 }
+// non-temporal (last-use) streaming load: the line is not kept in L2 / MALL
+__device__ __forceinline__ void load8_nt(const __bf16* p, float (&v)[8]) {
+  u16x8 a = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(p));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = __uint_as_float(((uint32_t)a[j]) << 16);
+}
 __device__ __forceinline__ void load8(const _Float16* p, float (&v)[8]) {
   u16x8 a = *reinterpret_cast<const u16x8*>(p);
 #pragma unroll
