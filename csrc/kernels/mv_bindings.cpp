@@ -351,7 +351,7 @@ at::Tensor bn_stats(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional
 std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
                                c10::optional<at::Tensor> y, at::Tensor vec,
                                c10::optional<at::Tensor> gamma, bool need_affine_grad,
-                               c10::optional<at::Tensor> dy2) {
+                               c10::optional<at::Tensor> dy2, int64_t dy2_stride) {
   int64_t C, C2;
   const int64_t M = bn_check_act(x, "x", &C);
   bn_check_act(dy, "grad", &C2);
@@ -369,9 +369,20 @@ std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
   const void* dy2p = nullptr;
   if (dy2.has_value() && dy2->defined()) {
     TORCH_CHECK(mode == 2, "bn: a second gradient stream is supported for mode 2 only");
-    TORCH_CHECK(dy2->sizes() == x.sizes() && dy2->strides() == x.strides() &&
-                dy2->scalar_type() == at::kBFloat16 && dy2->is_cuda(),
-                "bn: dy2 must match x in shape, layout and dtype");
+    TORCH_CHECK(dy2_stride >= 1, "bn: bad dy2 stride");
+    if (dy2_stride == 1) {
+      TORCH_CHECK(dy2->sizes() == x.sizes() && dy2->strides() == x.strides() &&
+                  dy2->scalar_type() == at::kBFloat16 && dy2->is_cuda(),
+                  "bn: dy2 must match x in shape, layout and dtype");
+    } else {
+      const int64_t s = dy2_stride;
+      TORCH_CHECK(x.dim() == 4 && dy2->dim() == 4 && dy2->size(0) == x.size(0) &&
+                  dy2->size(1) == x.size(1) && dy2->size(2) == (x.size(2) + s - 1) / s &&
+                  dy2->size(3) == (x.size(3) + s - 1) / s &&
+                  dy2->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dy2->scalar_type() == at::kBFloat16 && dy2->is_cuda(),
+                  "bn: strided dy2 must be channels_last bf16 [N, C, ceil(H/s), ceil(W/s)]");
+    }
     dy2p = dy2->data_ptr();
   }
   c10::DeviceGuard guard(x.device());
@@ -387,7 +398,8 @@ std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
             opt_f32(gamma, C, "weight"), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
             work[0].data_ptr<float>(), work[1].data_ptr<float>(), partial.data_ptr<float>(), P,
             work[2].data_ptr<float>(), work[3].data_ptr<float>(), work[4].data_ptr<float>(),
-            cur_stream());
+            dy2p ? (int)dy2_stride : 1, x.dim() == 4 ? (int)x.size(2) : 1,
+            x.dim() == 4 ? (int)x.size(3) : 1, cur_stream());
   at::Tensor dg, db;
   if (need_affine_grad) {
     dg = work[0];

@@ -21,4 +21,6 @@ void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const v
                int64_t M, int C, const float* save_mean, const float* save_invstd,
                const float* gamma, const float* scale, const float* bias, float* dgamma,
                float* dbeta, float* partial, int P, float* ca, float* cb, float* cc,
-               hipStream_t st);
+               int dy2_stride, int H, int W, hipStream_t st);
+// dy2_stride > 1: dy2 is [N, ceil(H/s), ceil(W/s), C] (gradient of a stride-s 1x1 conv's
+// input at its output resolution), added only on rows of the stride grid

@@ -56,6 +56,30 @@ __device__ __forceinline__ void ldlast(const __bf16* p, float (&v)[8]) {
   else load8(p, v);
 }
 
+// Second gradient stream of row r.  ds == 1: same [M, C] layout as dy.  ds > 1: dy2
+// is the gradient of a stride-ds 1x1 conv's input computed at the OUTPUT resolution
+// ([N, ceil(H/ds), ceil(W/ds), C]); rows off the stride grid get zero (the shortcut
+// downsample of a ResNet stage: no full-resolution zero-filled tensor exists).
+template <bool NT>
+__device__ __forceinline__ void ld_dy2(const __bf16* dy2, int64_t r, int c, int C, int ds,
+                                       int H, int W, float (&v)[8]) {
+  if (ds == 1) {
+    ldlast<NT>(dy2 + r * C + c, v);
+    return;
+  }
+  const int w = (int)(r % W);
+  const int64_t t = r / W;
+  const int h = (int)(t % H);
+  const int64_t n = t / H;
+  if ((h % ds) | (w % ds)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    return;
+  }
+  const int Ho = (H + ds - 1) / ds, Wo = (W + ds - 1) / ds;
+  ldlast<NT>(dy2 + ((n * Ho + h / ds) * Wo + w / ds) * C + c, v);
+}
+
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = p[j];
@@ -267,7 +291,8 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
     const __bf16* __restrict__ dy, const __bf16* __restrict__ dy2, const __bf16* __restrict__ x,
     const __bf16* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ scale,
-    const float* __restrict__ bias, __bf16* __restrict__ dz, float* __restrict__ partial, Geo g) {
+    const float* __restrict__ bias, __bf16* __restrict__ dz, float* __restrict__ partial, Geo g,
+    int ds, int H, int W) {
   int tc, tr, c;
   bool valid;
   lane_map(g, &tc, &tr, &c, &valid);
@@ -287,8 +312,8 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
       if (MODE == 2) ldlast<NT>(dy + o1, a1); else load8(dy + o1, a1);
       if (dy2) {   // second gradient stream of a tapped output (uniform branch)
         float b0[8], b1[8];
-        ldlast<NT>(dy2 + o0, b0);
-        ldlast<NT>(dy2 + o1, b1);
+        ld_dy2<NT>(dy2, r, c, g.C, ds, H, W, b0);
+        ld_dy2<NT>(dy2, r + g.RPI, c, g.C, ds, H, W, b1);
 #pragma unroll
         for (int j = 0; j < 8; ++j) { a0[j] += b0[j]; a1[j] += b1[j]; }
       }
@@ -310,7 +335,7 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
       if (MODE == 2) ldlast<NT>(dy + o0, a0); else load8(dy + o0, a0);
       if (dy2) {
         float b0[8];
-        ldlast<NT>(dy2 + o0, b0);
+        ld_dy2<NT>(dy2, r, c, g.C, ds, H, W, b0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) a0[j] += b0[j];
       }
@@ -558,18 +583,18 @@ template <int MODE>
 static int launch_bwd_reduce(const __bf16* dy, const __bf16* dy2, const __bf16* x,
                              const __bf16* y, const float* mean, const float* scale,
                              const float* bias, __bf16* dz, float* partial, int P, int64_t M,
-                             int C, hipStream_t st) {
+                             int C, int ds, int H, int W, hipStream_t st) {
   if (bn_nt()) {
     Geo gr = reduce_geo(M, C, P, (const void*)&bwd_reduce_kernel<MODE, true>);
     dim3 grr = grid_of(gr);
     hipLaunchKernelGGL((bwd_reduce_kernel<MODE, true>), grr, dim3(kBlock), 0, st, dy, dy2, x, y,
-                       mean, scale, bias, dz, partial, gr);
+                       mean, scale, bias, dz, partial, gr, ds, H, W);
     return (int)grr.x;
   }
   Geo gr = reduce_geo(M, C, P, (const void*)&bwd_reduce_kernel<MODE, false>);
   dim3 grr = grid_of(gr);
   hipLaunchKernelGGL((bwd_reduce_kernel<MODE, false>), grr, dim3(kBlock), 0, st, dy, dy2, x, y,
-                     mean, scale, bias, dz, partial, gr);
+                     mean, scale, bias, dz, partial, gr, ds, H, W);
   return (int)grr.x;
 }
 
@@ -592,7 +617,7 @@ void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const v
                int64_t M, int C, const float* save_mean, const float* save_invstd,
                const float* gamma, const float* scale, const float* bias, float* dgamma,
                float* dbeta, float* partial, int P, float* ca, float* cb, float* cc,
-               hipStream_t st) {
+               int dy2_stride, int H, int W, hipStream_t st) {
   const __bf16* dyp = (const __bf16*)dy;
   const __bf16* dy2p = (const __bf16*)dy2;
   const __bf16* xp = (const __bf16*)x;
@@ -600,9 +625,9 @@ void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const v
   __bf16* dzp = (__bf16*)dz;
   int pa;
   switch (mode) {
-    case 0: pa = launch_bwd_reduce<0>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, st); break;
-    case 1: pa = launch_bwd_reduce<1>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, st); break;
-    default: pa = launch_bwd_reduce<2>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, st); break;
+    case 0: pa = launch_bwd_reduce<0>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, dy2_stride, H, W, st); break;
+    case 1: pa = launch_bwd_reduce<1>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, dy2_stride, H, W, st); break;
+    default: pa = launch_bwd_reduce<2>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, dy2_stride, H, W, st); break;
   }
   hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
                      partial, pa, M, C, save_mean, save_invstd, gamma, dgamma, dbeta, ca, cb, cc);

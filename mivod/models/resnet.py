@@ -17,7 +17,8 @@ import os
 import torch.nn.functional as F
 
 from ..ops.conv import Conv2d
-from ..ops.bn import BatchNorm2d, bn_relu_maxpool, global_avg_pool, pad_channels, tap
+from ..ops.bn import (BatchNorm2d, bn_relu_maxpool, downsample_tap, global_avg_pool,
+                      pad_channels, tap)
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -63,9 +64,13 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         # the shortcut's gradient is added inside the backward of the op that
-        # produced x (mivod.ops.bn.tap), not by a separate autograd add
-        src = tap(x)
-        identity = src if self.downsample is None else self.downsample(src)
+        # produced x (mivod.ops.bn.tap), not by a separate autograd add; a strided
+        # 1x1 shortcut conv hands it over at its output resolution (downsample_tap)
+        if self.downsample is None:
+            identity = tap(x)
+        else:
+            conv, rest = self.downsample[0], self.downsample[1:]
+            identity = rest(downsample_tap(x, conv))
         out = self.bn1(self.conv1(x), relu=True)
         out = self.bn2(self.conv2(out), relu=True)
         # fused: relu(bn3(conv3(out)) + identity) in one pass (mivod.ops.bn)

@@ -43,14 +43,28 @@ class GradSlot:
     (1 extra read).  Autograd still orders the producer after the tap: a None
     gradient satisfies the dependency edge.
     """
-    __slots__ = ("grad",)
+    __slots__ = ("grad", "stride", "full_shape")
 
     def __init__(self):
         self.grad = None
+        self.stride = 1          # > 1: grad is on the stride-s grid (downsample_tap)
+        self.full_shape = None   # the tapped output's shape when stride > 1
 
     def take(self):
         g, self.grad = self.grad, None
+        if g is not None and self.stride > 1:      # a consumer without strided support
+            s, self.stride = self.stride, 1
+            full = torch.zeros(self.full_shape, dtype=g.dtype, device=g.device).contiguous(
+                memory_format=torch.channels_last)
+            full[:, :, ::s, ::s] = g
+            return full
         return g
+
+    def take_strided(self):
+        """(grad, stride) for kernels that read a stride-grid gradient directly."""
+        g, s = self.grad, self.stride
+        self.grad, self.stride = None, 1
+        return g, s
 
 
 class _Tap(torch.autograd.Function):
@@ -63,8 +77,57 @@ class _Tap(torch.autograd.Function):
     def backward(ctx, g):
         if g.dim() == 4:
             g = g.contiguous(memory_format=torch.channels_last)
+        assert ctx.slot.stride == 1, "a tapped output has one shortcut consumer"
         ctx.slot.grad = g if ctx.slot.grad is None else ctx.slot.grad + g
         return None, None
+
+
+class _DownsampleTapConv(torch.autograd.Function):
+    """Shortcut ``conv1x1(x, stride=s)`` of a tapped output (ResNet stage entry).
+    Backward: dW from the backward-weights solver; the input gradient is computed
+    at the OUTPUT resolution as a forward 1x1 conv with the transposed filter and
+    parked in x's producer slot with ``stride = s`` — the producer's BN backward
+    kernel adds it on the stride grid.  No full-resolution zero-filled gradient
+    (MIOpen strided backward-data: fill + scatter) is ever materialised."""
+
+    @staticmethod
+    def forward(ctx, x, w, s, slot):
+        ctx.save_for_backward(x, w)
+        ctx.s, ctx.slot = s, slot
+        return F.conv2d(x, w, None, s)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dw = None
+        if ctx.needs_input_grad[0]:
+            wt = w.transpose(0, 1).contiguous(memory_format=torch.channels_last)
+            assert ctx.slot.grad is None, "a tapped output has one shortcut consumer"
+            ctx.slot.grad = F.conv2d(dy, wt).contiguous(memory_format=torch.channels_last)
+            ctx.slot.stride = ctx.s
+            ctx.slot.full_shape = x.shape
+        if ctx.needs_input_grad[1]:
+            _, dw, _ = torch.ops.aten.convolution_backward(
+                dy, x, w, None, [ctx.s, ctx.s], [0, 0], [1, 1], False, [0, 0], 1,
+                [False, True, False])
+        return None, dw, None, None
+
+
+def downsample_tap(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """``conv(tap(x))`` for a 1x1 strided shortcut conv, fused as _DownsampleTapConv
+    when x's producer reads strided second gradients (fused BN, mode 2)."""
+    slot = getattr(x, "_mv_slot", None)
+    s = conv.stride[0]
+    if (slot is None or not (torch.is_grad_enabled() and x.requires_grad)
+            or os.environ.get("MIVOD_BN_TAP", "1") == "0"
+            or os.environ.get("MIVOD_DOWNSAMPLE_TAP", "1") == "0"
+            or tuple(conv.kernel_size) != (1, 1) or conv.stride[1] != s or s == 1
+            or tuple(conv.padding) != (0, 0) or conv.bias is not None or conv.groups != 1
+            or x.dtype != torch.bfloat16 or conv.weight.dtype != torch.bfloat16
+            or not x.is_contiguous(memory_format=torch.channels_last)):
+        return conv(tap(x))
+    return _DownsampleTapConv.apply(x, conv.weight, s, slot)
 
 
 def tap(x: torch.Tensor) -> torch.Tensor:
@@ -95,10 +158,12 @@ class _BNActTrain(torch.autograd.Function):
         x, y, vec, weight = ctx.saved_tensors
         dy = _cl(dy)
         need_affine = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
-        dy2 = ctx.slot.take() if ctx.slot is not None else None
+        dy2, s2 = None, 1
+        if ctx.slot is not None:
+            dy2, s2 = ctx.slot.take_strided() if ctx.mode == 2 else (ctx.slot.take(), 1)
         if dy2 is not None and ctx.mode != 2:
             dy, dy2 = dy + dy2, None
-        dx, dg, db, dz = K.native().bn_bwd(ctx.mode, dy, x, y, vec, weight, need_affine, dy2)
+        dx, dg, db, dz = K.native().bn_bwd(ctx.mode, dy, x, y, vec, weight, need_affine, dy2, s2)
         dres = None
         if ctx.has_res and ctx.needs_input_grad[8]:
             dres = dz if ctx.mode == 2 else dy
@@ -191,7 +256,7 @@ class _BNReluMaxPool(torch.autograd.Function):
         k, s, p = ctx.win
         dmid = nat.maxpool_bwd(_cl(dy), ctx.slot.take(), idx, x.shape[2], x.shape[3], k, s, p)
         need_affine = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
-        dx, dg, db, _ = nat.bn_bwd(1, dmid, x, None, vec, weight, need_affine, None)
+        dx, dg, db, _ = nat.bn_bwd(1, dmid, x, None, vec, weight, need_affine, None, 1)
         return (dx if ctx.needs_input_grad[0] else None,
                 dg if ctx.needs_input_grad[1] else None,
                 db if ctx.needs_input_grad[2] else None,

@@ -66,9 +66,9 @@ def test_bn_bwd_second_stream_equals_sum(cuda):
     b = torch.randn(64, device=cuda) * 0.1
     y, vec = nat.bn_fwd_train(x, g, b, None, None, 0.1, 1e-5, True, r)
     dy, dy2 = _cl(torch.randn_like(x)), _cl(torch.randn_like(x))
-    one = nat.bn_bwd(2, dy, x, y, vec, g, True, dy2)
+    one = nat.bn_bwd(2, dy, x, y, vec, g, True, dy2, 1)
     ref = nat.bn_bwd(2, _cl((dy.float() + dy2.float()).to(torch.bfloat16)), x, y, vec, g, True,
-                     None)
+                     None, 1)
     # the reference rounds dy + dy2 to bf16 before reducing; the fused kernel sums in
     # fp32, so the C-vectors (sums over 1568 rows) differ by ~sqrt(M) rounding steps
     for a, c, tol in zip(one, ref, (3e-2, 0.3, 0.3, 3e-2)):
@@ -155,3 +155,26 @@ def test_conv_dgrad_as_forward_matches_fp32(cuda, cin, cout, k, hw):
     for got, ref in ((y, y32), (x.grad, x32.grad), (m.weight.grad, w32.grad)):
         rel = (got.float() - ref).norm() / ref.norm()
         assert rel < 1e-2, rel
+
+
+
+def test_bn_bwd_strided_second_gradient(cuda):
+    """dy2 given at the stride-2 output resolution (a downsample conv's input gradient)
+    == the same gradient scattered onto the full-resolution grid with zeros."""
+    nat = K.native()
+    torch.manual_seed(3)
+    for (N, C, H, W) in ((2, 64, 14, 14), (3, 256, 7, 7)):
+        x = _cl(torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16))
+        r = _cl(torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16))
+        g = torch.rand(C, device=cuda) + 0.5
+        b = torch.randn(C, device=cuda) * 0.1
+        y, vec = nat.bn_fwd_train(x, g, b, None, None, 0.1, 1e-5, True, r)
+        dy = _cl(torch.randn_like(x))
+        Ho, Wo = (H + 1) // 2, (W + 1) // 2
+        dys = _cl(torch.randn(N, C, Ho, Wo, device=cuda).to(torch.bfloat16))
+        full = torch.zeros_like(x)
+        full[:, :, ::2, ::2] = dys
+        got = nat.bn_bwd(2, dy, x, y, vec, g, True, dys, 2)
+        ref = nat.bn_bwd(2, dy, x, y, vec, g, True, _cl(full), 1)
+        for a, c in zip(got, ref):
+            assert torch.equal(a, c)
