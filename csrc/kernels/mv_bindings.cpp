@@ -376,6 +376,7 @@ std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
                   "bn: dy2 must match x in shape, layout and dtype");
     } else {
       const int64_t s = dy2_stride;
+      TORCH_CHECK(M < (int64_t(1) << 32), "bn: strided dy2 needs fewer than 2^32 rows");
       TORCH_CHECK(x.dim() == 4 && dy2->dim() == 4 && dy2->size(0) == x.size(0) &&
                   dy2->size(1) == x.size(1) && dy2->size(2) == (x.size(2) + s - 1) / s &&
                   dy2->size(3) == (x.size(3) + s - 1) / s &&
@@ -645,6 +646,8 @@ at::Tensor maxpool_bwd(at::Tensor dy, c10::optional<at::Tensor> dy2, at::Tensor 
               "maxpool_bwd: output size does not match the window");
   TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.is_contiguous() &&
               idx.numel() == dy.numel(), "maxpool_bwd: idx must be uint8 [N, OH, OW, C]");
+  TORCH_CHECK(N * H * W * (C / 8) < (int64_t(1) << 32),
+              "maxpool_bwd: the kernel indexes N*H*W*C/8 lanes in 32 bits");
   const void* d2 = nullptr;
   if (dy2.has_value() && dy2->defined()) {
     check_nhwc(*dy2, "dy2");

@@ -67,17 +67,19 @@ __device__ __forceinline__ void ld_dy2(const __bf16* dy2, int64_t r, int c, int 
     ldlast<NT>(dy2 + r * C + c, v);
     return;
   }
-  const int w = (int)(r % W);
-  const int64_t t = r / W;
-  const int h = (int)(t % H);
-  const int64_t n = t / H;
-  if ((h % ds) | (w % ds)) {
+  // 32-bit index math (the launcher guarantees M < 2^32): a 64-bit divide per row
+  // costs ~100 ALU instructions per lane, comparable to the load itself
+  const uint32_t r32 = (uint32_t)r, W32 = (uint32_t)W, H32 = (uint32_t)H;
+  const uint32_t t = r32 / W32, w = r32 - t * W32;
+  const uint32_t n = t / H32, h = t - n * H32;
+  if ((h % (uint32_t)ds) | (w % (uint32_t)ds)) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = 0.f;
     return;
   }
-  const int Ho = (H + ds - 1) / ds, Wo = (W + ds - 1) / ds;
-  ldlast<NT>(dy2 + ((n * Ho + h / ds) * Wo + w / ds) * C + c, v);
+  const uint32_t Ho = (H32 + ds - 1) / ds, Wo = (W32 + ds - 1) / ds;
+  const int64_t ro = ((int64_t)(n * Ho + h / ds)) * Wo + w / ds;
+  ldlast<NT>(dy2 + ro * C + c, v);
 }
 
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {

@@ -88,12 +88,16 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restri
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)g.N * g.H * g.W * cv;
   if (t >= total) return;
-  const int c = (int)(t % cv) * 8;
-  int64_t pix = t / cv;
-  const int iw = (int)(pix % g.W);
-  pix /= g.W;
-  const int ih = (int)(pix % g.H);
-  const int n = (int)(pix / g.H);
+  // 32-bit index math (launcher: total < 2^32): 64-bit div/mod per lane was the
+  // kernel's bottleneck (~2 TB/s)
+  const uint32_t t32 = (uint32_t)t, cv32 = (uint32_t)cv;
+  const uint32_t pix0 = t32 / cv32;
+  const int c = (int)(t32 - pix0 * cv32) * 8;
+  const uint32_t pw = pix0 / (uint32_t)g.W;
+  const int iw = (int)(pix0 - pw * (uint32_t)g.W);
+  const uint32_t ph = pw / (uint32_t)g.H;
+  const int ih = (int)(pw - ph * (uint32_t)g.H);
+  const int n = (int)ph;
   // output windows containing ih: oh*s - p <= ih <= oh*s - p + k - 1
   const int ohl = max(0, (ih + g.p - g.k + g.s) / g.s);
   const int ohh = min(g.OH - 1, (ih + g.p) / g.s);
@@ -217,6 +221,7 @@ void mv_maxpool_bwd(const void* dy, const void* dy2, const uint8_t* idx, void* d
   PoolGeo g{N, H, W, C, OH, OW, k, s, p};
   const int64_t total = (int64_t)N * H * W * (C / 8);
   if (!total) return;
+  if (total >= (int64_t(1) << 32)) return;   // bindings reject such shapes first
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
                      (const __bf16*)dy, (const __bf16*)dy2, idx, (__bf16*)dx, g);
 }
