@@ -435,8 +435,9 @@ __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict_
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] *= scale;
-  const int64_t row = i / D, d = i % D;          // row = (b*s + q)*h + hi
-  const int64_t bsq = row / h, hi = row % h;
+  const int64_t row = i / D, d = i % D;          // row = (b*s + q)*h + hi (D: power of 2)
+  const uint32_t r32 = (uint32_t)row, bsq32 = r32 / (uint32_t)h;   // rows < 2^32 (bindings)
+  const int64_t bsq = bsq32, hi = r32 - bsq32 * (uint32_t)h;
   store8(dqkv + bsq * 3 * h * D + hi * D + d, acc);
 }
 

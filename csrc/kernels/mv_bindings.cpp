@@ -457,6 +457,7 @@ at::Tensor attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor 
               out.numel() == (int64_t)p.b * p.s * p.h * 64 &&
               dout.scalar_type() == at::kBFloat16, "attn_bwd: out/dout must be bf16 [b,s,h,64]");
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)p.b * p.h * p.s, "attn_bwd: lse");
+  TORCH_CHECK((int64_t)p.b * p.s * p.h < (int64_t(1) << 32), "attn_bwd: b*s*h must be < 2^32");
   p.lse = lse.data_ptr<float>();
   auto fo = qkv.options().dtype(at::kFloat);
   const int nkb = (p.s + 63) / 64;
@@ -623,6 +624,8 @@ std::vector<at::Tensor> maxpool_fwd(at::Tensor x, c10::optional<at::Tensor> scal
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
   TORCH_CHECK(OH > 0 && OW > 0, "maxpool: empty output");
+  TORCH_CHECK(N * OH * OW * (C / 8) < (int64_t(1) << 32),
+              "maxpool: the kernel indexes N*OH*OW*C/8 lanes in 32 bits");
   const float* sp = nullptr;
   const float* bp = nullptr;
   if (scale.has_value() && scale->defined()) {
@@ -675,6 +678,8 @@ at::Tensor gap_bwd(at::Tensor dy, int64_t H, int64_t W) {
               dy.is_contiguous() && dy.size(1) % 8 == 0, "gap_bwd: dy must be bf16 [N, C]");
   c10::DeviceGuard guard(dy.device());
   const int64_t N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(N * H * W * (C / 8) < (int64_t(1) << 32),
+              "gap_bwd: the kernel indexes N*H*W*C/8 lanes in 32 bits");
   at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   mv_gap_bwd(dy.data_ptr(), dx.data_ptr(), (int)N, (int)(H * W), (int)C, cur_stream());
   return dx;

@@ -34,12 +34,15 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restri
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)g.N * g.OH * g.OW * cv;
   if (t >= total) return;
-  const int c = (int)(t % cv) * 8;
-  int64_t pix = t / cv;
-  const int ow = (int)(pix % g.OW);
-  pix /= g.OW;
-  const int oh = (int)(pix % g.OH);
-  const int n = (int)(pix / g.OH);
+  // 32-bit index math (launcher: total < 2^32); 64-bit div/mod per lane is ~100 ALU ops
+  const uint32_t t32 = (uint32_t)t, cv32 = (uint32_t)cv;
+  const uint32_t pix0 = t32 / cv32;
+  const int c = (int)(t32 - pix0 * cv32) * 8;
+  const uint32_t pw = pix0 / (uint32_t)g.OW;
+  const int ow = (int)(pix0 - pw * (uint32_t)g.OW);
+  const uint32_t ph = pw / (uint32_t)g.OH;
+  const int oh = (int)(pw - ph * (uint32_t)g.OH);
+  const int n = (int)ph;
   float sc[8], bi[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sc[j] = 1.f; bi[j] = 0.f; }
@@ -166,8 +169,10 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const __bf16* __restrict__
   const int cv = C / 8;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)N * HW * cv) return;
-  const int c = (int)(t % cv) * 8;
-  const int n = (int)(t / ((int64_t)HW * cv));
+  const uint32_t t32 = (uint32_t)t, cv32 = (uint32_t)cv;   // launcher: total < 2^32
+  const uint32_t q = t32 / cv32;
+  const int c = (int)(t32 - q * cv32) * 8;
+  const int n = (int)(q / (uint32_t)HW);
   float v[8];
   load8(dy + (int64_t)n * C + c, v);
   const float inv = 1.f / (float)HW;
@@ -211,6 +216,7 @@ void mv_maxpool_fwd(const void* x, const float* scale, const float* bias, bool r
                     hipStream_t st) {
   PoolGeo g{N, H, W, C, OH, OW, k, s, p};
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  if (total >= (int64_t(1) << 32)) return;   // bindings reject such shapes first
   if (!total) return;
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
                      (const __bf16*)x, scale, bias, relu ? 1 : 0, (__bf16*)y, idx, g);
@@ -235,7 +241,7 @@ void mv_gap_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st) {
 
 void mv_gap_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st) {
   const int64_t total = (int64_t)N * HW * (C / 8);
-  if (!total) return;
+  if (!total || total >= (int64_t(1) << 32)) return;   // bindings reject such shapes first
   hipLaunchKernelGGL(gap_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
                      (const __bf16*)dy, (__bf16*)dx, N, HW, C);
 }
