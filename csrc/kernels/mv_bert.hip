@@ -58,7 +58,21 @@ __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const __bf16* __rest
   load8(b + c, bv);
   const int64_t r0 = blockIdx.x * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
-  for (int64_t r = r0; r < r1; ++r) {
+  int64_t r = r0;
+  // 4 rows per step: 4 independent 16-B loads in flight per lane (one row at a time
+  // left the lane waiting on each load's full latency: ~4 TB/s)
+  for (; r + 3 < r1; r += 4) {
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load8(x + (r + u) * N + c, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[u][j] = gelu(v[u][j] + bv[j]);
+      store8(y + (r + u) * N + c, v[u]);
+    }
+  }
+  for (; r < r1; ++r) {
     float v[8];
     load8(x + r * N + c, v);
 #pragma unroll
@@ -82,7 +96,25 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const __bf16* __rest
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   const int64_t r0 = blockIdx.x * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
-  for (int64_t r = r0; r < r1; ++r) {
+  int64_t r = r0;
+  for (; r + 1 < r1; r += 2) {   // 2 rows x 2 tensors = 4 loads in flight per lane
+    float v[2][8], g[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      load8(x + (r + u) * N + c, v[u]);
+      load8(dy + (r + u) * N + c, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        g[u][j] *= gelu_grad(v[u][j] + bv[j]);
+        acc[j] += g[u][j];
+      }
+      store8(dx + (r + u) * N + c, g[u]);
+    }
+  }
+  for (; r < r1; ++r) {
     float v[8], g[8];
     load8(x + r * N + c, v);
     load8(dy + r * N + c, g);
