@@ -75,6 +75,13 @@ def parse():
     return ap.parse_args()
 
 
+def _transport(size: int) -> str:
+    from mivod.common import basics
+    if size == 1:
+        return "local"
+    return "rccl" if basics.state().backend == "nccl" else basics.state().backend
+
+
 def main():
     args = parse()
     import torch
@@ -149,7 +156,10 @@ def main():
     def barrier():
         if size > 1:
             import torch.distributed as dist
-            dist.barrier(device_ids=[dev.index])
+            if dist.get_backend() == "nccl":
+                dist.barrier(device_ids=[dev.index])
+            else:                      # MIVOD_TRANSPORT=gloo-gpu rehearsal (ranks share a GPU)
+                dist.barrier()
         torch.cuda.synchronize()
 
     barrier()
@@ -191,7 +201,7 @@ def main():
                 "parallelism": f"dp{size}",
                 "optimizer": f"mivod Fused{args.optimizer.upper()} via DistributedOptimizer",
                 "compression": args.compression,
-                "transport": "rccl" if size > 1 else "local",
+                "transport": _transport(size),
                 "hip_graph": bool(args.graph),
             },
         }

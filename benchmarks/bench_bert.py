@@ -78,14 +78,20 @@ def main():
                   flush=True)
     torch.cuda.synchronize()
     if size > 1:
-        torch.distributed.barrier(device_ids=[dev.index])
+        if torch.distributed.get_backend() == "nccl":
+            torch.distributed.barrier(device_ids=[dev.index])
+        else:
+            torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
     if size > 1:
-        torch.distributed.barrier(device_ids=[dev.index])
+        if torch.distributed.get_backend() == "nccl":
+            torch.distributed.barrier(device_ids=[dev.index])
+        else:
+            torch.distributed.barrier()
     el = time.perf_counter() - t0
     if size > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
