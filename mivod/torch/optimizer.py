@@ -242,10 +242,32 @@ class _DistributedOptimizerMixin:
             self._mvd_autotune = BucketAutotuner(log_path=cfg.autotune_log)
             f0, b0 = self._mvd_autotune.current()
             self._mvd_replan(f0, b0)
+        if st.size > 1:
+            self._mvd_check_schedule()
         self._mvd_hooks = []
         for p in trainable:
             self._mvd_hooks.append(p.register_post_accumulate_grad_hook(self._mvd_hook))
         TL.note_plan(self._mvd_buckets)
+
+    def _mvd_check_schedule(self):
+        """Every rank must issue the same collectives in the same order: compare a
+        64-bit hash of the static bucket plan (names, element counts, dtypes, op,
+        compression) across ranks once, and raise on ALL ranks if they differ —
+        instead of mismatched RCCL calls hanging or silently mixing tensors."""
+        import hashlib
+        h = hashlib.blake2b(digest_size=8)
+        h.update(repr((C.op_name(self._mvd_op), self._mvd_compression.__name__,
+                       self._mvd_bpps)).encode())
+        for b in self._mvd_buckets:
+            h.update(repr((str(b.arena.grad.dtype), b.hi - b.lo,
+                           [(self._mvd_names[id(p)], tuple(p.shape)) for p in b.params])).encode())
+        v = int.from_bytes(h.digest(), "little", signed=True)
+        every = C.allgather(torch.tensor([v], dtype=torch.int64))   # CPU: native ring / gloo
+        if not bool((every == every[0]).all()):
+            raise ValueError(
+                "mivod DistributedOptimizer: the static gradient schedule differs across ranks "
+                f"(plan hashes {sorted(set(every.tolist()))}); every rank must wrap the same "
+                "model with the same parameter order, dtypes, op, compression and bucket settings")
 
     # --------------------------------------------------------------- hot path
     def _mvd_hook(self, p: torch.Tensor):

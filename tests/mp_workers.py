@@ -540,6 +540,26 @@ def gpu_adasum():
     print("OK", r)
 
 
+def schedule_mismatch():
+    """Rank 1 wraps a different model: every rank raises (no hang, no silent mixing)."""
+    hvd.init()
+    r = hvd.rank()
+    m = torch.nn.Linear(4, 4) if r == 0 else torch.nn.Linear(4, 5)
+    try:
+        hvd.DistributedOptimizer(torch.optim.SGD(m.parameters(), lr=0.1),
+                                 named_parameters=m.named_parameters())
+    except ValueError as e:
+        assert "schedule differs across ranks" in str(e), e
+        print("raised", r)
+    else:
+        raise AssertionError("schedule mismatch not detected")
+    m2 = torch.nn.Linear(4, 4)
+    hvd.DistributedOptimizer(torch.optim.SGD(m2.parameters(), lr=0.1),
+                             named_parameters=m2.named_parameters())   # equal plans pass
+    hvd.shutdown()
+    print("OK", r)
+
+
 def hvd_rank():
     return int(os.environ.get("RANK", "0"))
 

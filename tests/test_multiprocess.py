@@ -106,3 +106,9 @@ def test_native_tcp_ring(n):
     """C++ ring allreduce / broadcast / allgatherv on CPU tensors (all dtypes incl.
     fp16 via F16C and bf16), bitwise identical across ranks, odd world sizes."""
     run_ranks("ring", n)
+
+
+def test_schedule_mismatch_raises_on_all_ranks():
+    """SURVEY §7.4 risk 4: a differing static bucket schedule raises everywhere."""
+    outs = run_ranks("schedule_mismatch", 2)
+    assert all(f"raised {r}" in o for r, o in enumerate(outs))
