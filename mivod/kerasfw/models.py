@@ -21,9 +21,11 @@ architecture + optimizer config in the metadata) whatever the extension
 """
 from __future__ import annotations
 
+import itertools
 import json
 import math
 import time
+import weakref
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -57,6 +59,12 @@ def _to_tensor(a, dev, dtype=None):
     return t.to(dev, non_blocking=True)
 
 
+# Live models in creation order: ``mivod.tensorflow.global_variables()`` (the
+# tf.global_variables() collection horovod's broadcast_global_variables walks).
+_LIVE_MODELS: "weakref.WeakSet" = weakref.WeakSet()
+_model_seq = itertools.count()
+
+
 class Model(nn.Module):
     """Keras-style model.  Subclass and implement ``call``, or use Sequential."""
 
@@ -71,6 +79,8 @@ class Model(nn.Module):
         self.history = None
         self._compiled = False
         self._dev = None
+        self._mvd_seq = next(_model_seq)
+        _LIVE_MODELS.add(self)
 
     @property
     def name(self):

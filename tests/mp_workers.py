@@ -560,6 +560,64 @@ def schedule_mismatch():
     print("OK", r)
 
 
+def tensorflow_api():
+    """``import horovod.tensorflow as hvd`` (U18): dense / IndexedSlices / sparse allreduce,
+    broadcast_global_variables over every live model, DistributedOptimizer.compute_gradients
+    and DistributedGradientTape return rank-averaged gradients."""
+    import horovod.tensorflow as htf
+    from mivod import kerasfw as keras
+    htf.init()
+    r, n = htf.rank(), htf.size()
+    x = torch.full((6,), float(r + 1))
+    _close(htf.allreduce(x), torch.full((6,), (n + 1) / 2.0))
+    _close(htf.allreduce(x, average=False), torch.full((6,), n * (n + 1) / 2.0))
+    _close(htf.allreduce(x, compression=htf.Compression.fp16), torch.full((6,), (n + 1) / 2.0),
+           tol=1e-3)
+    # IndexedSlices -> allgather of values + indices, values / size when averaging
+    sl = htf.IndexedSlices(torch.full((1, 3), float(r + 1)), torch.tensor([r]), (n, 3))
+    out = htf.allreduce(sl)
+    assert isinstance(out, htf.IndexedSlices) and out.indices.tolist() == list(range(n))
+    dense = out.to_dense()
+    for rr in range(n):
+        _close(dense[rr], torch.full((3,), (rr + 1) / n))
+    sp = torch.sparse_coo_tensor(torch.tensor([[0]]), torch.full((1, 2), 2.0), (n, 2))
+    d = htf.allreduce(sp, average=False)
+    assert d.is_sparse
+    _close(d.to_dense()[0], torch.full((2,), 2.0 * n))
+    # broadcast_global_variables: every live model (no model argument, as in TF1)
+    torch.manual_seed(100 + r)
+    m1 = keras.Sequential([keras.layers.Dense(4, input_shape=(3,))])
+    m1.build((None, 3))
+    m2 = keras.Sequential([keras.layers.Dense(2, input_shape=(5,))])
+    m2.build((None, 5))
+    htf.broadcast_global_variables(0)
+    gv = htf.global_variables()
+    assert len(gv) >= 4
+    flat = torch.cat([v.detach().reshape(-1) for v in gv])
+    allf = htf.allgather(flat.unsqueeze(0))
+    assert torch.equal(allf[0], allf[-1])
+    # DistributedOptimizer.compute_gradients: averaged; apply_gradients keeps ranks in sync
+    opt = htf.DistributedOptimizer(keras.optimizers.SGD(lr=0.1))
+    w = list(m1.trainable_weights)
+    inp = torch.full((2, 3), float(r + 1))
+    gv_pairs = opt.compute_gradients(m1(inp).sum(), w)
+    local = torch.autograd.grad(m1(inp).sum(), w)
+    every = htf.allgather(torch.cat([g.reshape(-1) for g in local]).unsqueeze(0))
+    _close(torch.cat([g.reshape(-1) for g, _ in gv_pairs]), every.mean(0))
+    opt.apply_gradients(gv_pairs)
+    flat = torch.cat([v.detach().reshape(-1) for v in m1.trainable_weights]).unsqueeze(0)
+    allf = htf.allgather(flat)
+    assert torch.equal(allf[0], allf[-1])
+    # DistributedGradientTape
+    v = torch.tensor([1.0, 2.0], requires_grad=True)
+    with htf.DistributedGradientTape(htf.GradientTape()) as tape:
+        loss = (v * float(r + 1)).sum()
+    g = tape.gradient(loss, v)
+    _close(g, torch.full((2,), (n + 1) / 2.0))
+    htf.shutdown()
+    print("OK", r)
+
+
 def hvd_rank():
     return int(os.environ.get("RANK", "0"))
 

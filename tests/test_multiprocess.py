@@ -101,6 +101,12 @@ def test_horovod_namespace_2ranks():
     run_ranks("horovod_namespace", 2)
 
 
+def test_horovod_tensorflow_api_2ranks():
+    """horovod.tensorflow surface (U18): sparse allreduce, global-variable broadcast,
+    DistributedOptimizer.compute_gradients, DistributedGradientTape."""
+    run_ranks("tensorflow_api", 2)
+
+
 @pytest.mark.parametrize("n", [2, 3, 4])
 def test_native_tcp_ring(n):
     """C++ ring allreduce / broadcast / allgatherv on CPU tensors (all dtypes incl.
