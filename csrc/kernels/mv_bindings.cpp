@@ -274,11 +274,14 @@ const float* opt_f32(const c10::optional<at::Tensor>& t, int64_t C, const char* 
   return t->data_ptr<float>();
 }
 
-std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> gamma,
-                                     c10::optional<at::Tensor> beta,
-                                     c10::optional<at::Tensor> running_mean,
-                                     c10::optional<at::Tensor> running_var, double momentum,
-                                     double eps, bool relu, c10::optional<at::Tensor> residual) {
+// want_mask (relu + residual only): also return the [M, C/8] uint8 bitmask of y > 0 that
+// backward mode 3 reads instead of y
+std::vector<at::Tensor> bn_fwd_train_impl(at::Tensor x, c10::optional<at::Tensor> gamma,
+                                          c10::optional<at::Tensor> beta,
+                                          c10::optional<at::Tensor> running_mean,
+                                          c10::optional<at::Tensor> running_var, double momentum,
+                                          double eps, bool relu,
+                                          c10::optional<at::Tensor> residual, bool want_mask) {
   int64_t C;
   const int64_t M = bn_check_act(x, "x", &C);
   TORCH_CHECK(M > 0, "bn: empty input");
@@ -296,6 +299,11 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> gam
   at::Tensor partial = at::empty({(int64_t)P * 2 * C}, fo);
   at::Tensor vec = at::empty({4, C}, fo);   // save_mean, save_invstd, scale, bias
   at::Tensor y = at::empty_like(x);
+  at::Tensor mask;
+  if (want_mask) {
+    TORCH_CHECK(relu && rp != nullptr, "bn: the output bitmask needs relu and a residual");
+    mask = at::empty({M, C / 8}, x.options().dtype(at::kByte));
+  }
   float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
   float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
   TORCH_CHECK((rm == nullptr) == (rv == nullptr), "bn: running_mean/var must both be given");
@@ -303,8 +311,28 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> gam
                   opt_f32(beta, C, "bias"), (float)momentum, (float)eps, relu,
                   partial.data_ptr<float>(), P, vec[0].data_ptr<float>(),
                   vec[1].data_ptr<float>(), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
-                  cur_stream());
+                  cur_stream(), want_mask ? mask.data_ptr() : nullptr);
+  if (want_mask) return {y, vec, mask};
   return {y, vec};
+}
+
+std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> gamma,
+                                     c10::optional<at::Tensor> beta,
+                                     c10::optional<at::Tensor> running_mean,
+                                     c10::optional<at::Tensor> running_var, double momentum,
+                                     double eps, bool relu, c10::optional<at::Tensor> residual) {
+  return bn_fwd_train_impl(x, gamma, beta, running_mean, running_var, momentum, eps, relu,
+                           residual, false);
+}
+
+// {y, vec, mask}: add+ReLU forward that also records the backward bitmask (mode 3)
+std::vector<at::Tensor> bn_fwd_train_mask(at::Tensor x, c10::optional<at::Tensor> gamma,
+                                          c10::optional<at::Tensor> beta,
+                                          c10::optional<at::Tensor> running_mean,
+                                          c10::optional<at::Tensor> running_var, double momentum,
+                                          double eps, at::Tensor residual) {
+  return bn_fwd_train_impl(x, gamma, beta, running_mean, running_var, momentum, eps, true,
+                           residual, true);
 }
 
 at::Tensor bn_apply(at::Tensor x, at::Tensor scale, at::Tensor bias, bool relu,
@@ -347,7 +375,7 @@ at::Tensor bn_stats(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional
   return vec;
 }
 
-// returns {dx, dgamma, dbeta, dz}; dz defined only for mode 2 (residual branch grad)
+// returns {dx, dgamma, dbeta, dz}; dz defined only for modes 2 and 3 (residual branch grad)
 std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
                                c10::optional<at::Tensor> y, at::Tensor vec,
                                c10::optional<at::Tensor> gamma, bool need_affine_grad,
@@ -356,7 +384,7 @@ std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
   const int64_t M = bn_check_act(x, "x", &C);
   bn_check_act(dy, "grad", &C2);
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides(), "bn: grad layout mismatch");
-  TORCH_CHECK(mode >= 0 && mode <= 2, "bn: bad mode");
+  TORCH_CHECK(mode >= 0 && mode <= 3, "bn: bad mode");
   TORCH_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() &&
               vec.numel() == 4 * C, "bn: saved stats must be fp32 [4, C]");
   const void* yp = nullptr;
@@ -365,10 +393,15 @@ std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
                 y->strides() == x.strides() && y->scalar_type() == at::kBFloat16,
                 "bn: mode 2 needs the saved output");
     yp = y->data_ptr();
+  } else if (mode == 3) {
+    TORCH_CHECK(y.has_value() && y->defined() && y->is_cuda() && y->is_contiguous() &&
+                y->scalar_type() == at::kByte && y->dim() == 2 && y->size(0) == M &&
+                y->size(1) == C / 8, "bn: mode 3 needs the forward's [M, C/8] uint8 bitmask");
+    yp = y->data_ptr();
   }
   const void* dy2p = nullptr;
   if (dy2.has_value() && dy2->defined()) {
-    TORCH_CHECK(mode == 2, "bn: a second gradient stream is supported for mode 2 only");
+    TORCH_CHECK(mode >= 2, "bn: a second gradient stream is supported for modes 2 and 3 only");
     TORCH_CHECK(dy2_stride >= 1, "bn: bad dy2 stride");
     if (dy2_stride == 1) {
       TORCH_CHECK(dy2->sizes() == x.sizes() && dy2->strides() == x.strides() &&
@@ -393,8 +426,8 @@ std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
   at::Tensor work = at::empty({5, C}, fo);  // dgamma, dbeta, a, b, c
   at::Tensor dx = at::empty_like(x);
   at::Tensor dz;
-  if (mode == 2) dz = at::empty_like(x);
-  mv_bn_bwd((int)mode, dy.data_ptr(), dy2p, x.data_ptr(), yp, mode == 2 ? dz.data_ptr() : nullptr,
+  if (mode >= 2) dz = at::empty_like(x);
+  mv_bn_bwd((int)mode, dy.data_ptr(), dy2p, x.data_ptr(), yp, mode >= 2 ? dz.data_ptr() : nullptr,
             dx.data_ptr(), M, (int)C, vec[0].data_ptr<float>(), vec[1].data_ptr<float>(),
             opt_f32(gamma, C, "weight"), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
             work[0].data_ptr<float>(), work[1].data_ptr<float>(), partial.data_ptr<float>(), P,
@@ -725,6 +758,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("ln_fwd", &ln_fwd, "v = res + dropout(z + b); y = LN(v) -> (y, v, mean, rstd)");
   m.def("ln_bwd", &ln_bwd, "-> (dv, dz, dgamma, dbeta, dbias)");
   m.def("bn_fwd_train", &bn_fwd_train, "fused NHWC BN(+add)(+ReLU) training forward");
+  m.def("bn_fwd_train_mask", &bn_fwd_train_mask,
+        "fused NHWC BN+add+ReLU training forward that also returns the backward bitmask");
   m.def("bn_apply", &bn_apply, "NHWC y = act(x*scale + bias (+res))");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward (+ second grad stream)");
   m.def("bn_stats", &bn_stats, "NHWC BN training statistics only -> [4, C]");

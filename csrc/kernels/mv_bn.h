@@ -10,12 +10,14 @@ int mv_bn_partials(int64_t M, int C);
 void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, float* rmean,
                      float* rvar, const float* gamma, const float* beta, float momentum, float eps,
                      bool relu, float* partial, int P, float* save_mean, float* save_invstd,
-                     float* scale, float* bias, hipStream_t st);
+                     float* scale, float* bias, hipStream_t st, void* mask = nullptr);
 
 void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
-                 const float* bias, bool relu, hipStream_t st);
+                 const float* bias, bool relu, hipStream_t st, void* mask = nullptr);
+// mask (add+ReLU only, may be null): [M, C/8] bytes, bit j of byte (r, c/8) = y[r, c+j] > 0
 
-// mode 0: plain BN, 1: BN+ReLU (mask from x), 2: BN+add+ReLU (mask from y, writes dz).
+// mode 0: plain BN, 1: BN+ReLU (mask from x), 2: BN+add+ReLU (mask from y, writes dz),
+// 3: as 2 with y = the forward's [M, C/8] bitmask.
 // dy2 (mode 2 only, may be null): second gradient stream added to dy on the fly.
 void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const void* y, void* dz, void* dx,
                int64_t M, int C, const float* save_mean, const float* save_invstd,

@@ -219,16 +219,27 @@ __global__ __launch_bounds__(kBlock) void finalize_fwd_kernel(
   bias[ch] = (beta ? beta[ch] : 0.f) - mean * sc;
 }
 
+// bit j set <=> output channel c+j of the row is > 0 (the add+ReLU backward mask:
+// 1 byte per 8 channels instead of re-reading the 16-byte bf16 output)
+__device__ __forceinline__ uint8_t relu_bits(const float (&v)[8]) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m |= (v[j] > 0.f ? 1u : 0u) << j;
+  return (uint8_t)m;
+}
+
 template <bool RELU, bool RES, bool NT = true>
 __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict__ x,
                                                         const __bf16* __restrict__ res,
                                                         const float* __restrict__ scale,
                                                         const float* __restrict__ bias,
-                                                        __bf16* __restrict__ y, Geo g) {
+                                                        __bf16* __restrict__ y, Geo g,
+                                                        uint8_t* __restrict__ mask) {
   int tc, tr, c;
   bool valid;
   lane_map(g, &tc, &tr, &c, &valid);
   if (!valid) return;
+  const int C8 = g.C / kVec;
   float sc[8], bi[8];
   load8f(scale + c, sc);
   load8f(bias + c, bi);
@@ -252,6 +263,10 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict_
     }
     store8(y + o0, v0);
     store8(y + o1, v1);
+    if (RELU && RES && mask) {
+      mask[r * C8 + c / kVec] = relu_bits(v0);
+      mask[(r + g.RPI) * C8 + c / kVec] = relu_bits(v1);
+    }
   }
   for (; r < r1; r += g.RPI) {
     float v0[8], q0[8];
@@ -266,6 +281,7 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict_
       v0[j] = a;
     }
     store8(y + o0, v0);
+    if (RELU && RES && mask) mask[r * C8 + c / kVec] = relu_bits(v0);
   }
 }
 
@@ -274,13 +290,17 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict_
 // MODE 1: ReLU, mask recomputed from x:  d = (fma(x, scale, bias) > 0) ? dy : 0
 // MODE 2: add + ReLU, mask from the saved output y: d = (y > 0) ? dy : 0; d is
 //         written out (it is also the residual branch's gradient)
+// MODE 3: MODE 2 with the forward's 1-bit-per-channel mask ([M, C/8] bytes) in place
+//         of y: one byte per lane-row instead of a 16-byte bf16 load (~1/5 of the
+//         pass's HBM traffic)
 template <int MODE>
 __device__ __forceinline__ void masked(const float (&dy)[8], const float (&x)[8],
                                        const float (&yv)[8], const float (&sc)[8],
                                        const float (&bi)[8], float (&d)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    if (MODE == 0) d[j] = dy[j];
+    if (MODE == 3) d[j] = (__float_as_uint(yv[0]) >> j) & 1u ? dy[j] : 0.f;
+    else if (MODE == 0) d[j] = dy[j];
     else if (MODE == 1) d[j] = __builtin_fmaf(x[j], sc[j], bi[j]) > 0.f ? dy[j] : 0.f;
     else d[j] = yv[j] > 0.f ? dy[j] : 0.f;
   }
@@ -298,6 +318,9 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
   int tc, tr, c;
   bool valid;
   lane_map(g, &tc, &tr, &c, &valid);
+  constexpr bool DZ = MODE >= 2;   // writes the masked gradient (residual branch)
+  const uint8_t* mk = (const uint8_t*)y;
+  const int C8 = g.C / kVec;
   float s1[8], s2[8], mu[8], sc[8], bi[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; mu[j] = 0.f; sc[j] = 0.f; bi[j] = 0.f; }
@@ -310,8 +333,8 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
     for (; r + g.RPI < r1; r += 2 * g.RPI) {
       float a0[8], a1[8], x0[8], x1[8], y0[8], y1[8], d0[8], d1[8];
       const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
-      if (MODE == 2) ldlast<NT>(dy + o0, a0); else load8(dy + o0, a0);
-      if (MODE == 2) ldlast<NT>(dy + o1, a1); else load8(dy + o1, a1);
+      if (DZ) ldlast<NT>(dy + o0, a0); else load8(dy + o0, a0);
+      if (DZ) ldlast<NT>(dy + o1, a1); else load8(dy + o1, a1);
       if (dy2) {   // second gradient stream of a tapped output (uniform branch)
         float b0[8], b1[8];
         ld_dy2<NT>(dy2, r, c, g.C, ds, H, W, b0);
@@ -322,9 +345,13 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
       load8(x + o0, x0);
       load8(x + o1, x1);
       if (MODE == 2) { ldlast<NT>(y + o0, y0); ldlast<NT>(y + o1, y1); }
+      if (MODE == 3) {
+        y0[0] = __uint_as_float((uint32_t)mk[r * C8 + c / kVec]);
+        y1[0] = __uint_as_float((uint32_t)mk[(r + g.RPI) * C8 + c / kVec]);
+      }
       masked<MODE>(a0, x0, y0, sc, bi, d0);
       masked<MODE>(a1, x1, y1, sc, bi, d1);
-      if (MODE == 2) { store8(dz + o0, d0); store8(dz + o1, d1); }
+      if (DZ) { store8(dz + o0, d0); store8(dz + o1, d1); }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         s1[j] += d0[j] + d1[j];
@@ -334,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
     for (; r < r1; r += g.RPI) {
       float a0[8], x0[8], y0[8], d0[8];
       const int64_t o0 = r * g.C + c;
-      if (MODE == 2) ldlast<NT>(dy + o0, a0); else load8(dy + o0, a0);
+      if (DZ) ldlast<NT>(dy + o0, a0); else load8(dy + o0, a0);
       if (dy2) {
         float b0[8];
         ld_dy2<NT>(dy2, r, c, g.C, ds, H, W, b0);
@@ -343,8 +370,9 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
       }
       load8(x + o0, x0);
       if (MODE == 2) ldlast<NT>(y + o0, y0);
+      if (MODE == 3) y0[0] = __uint_as_float((uint32_t)mk[r * C8 + c / kVec]);
       masked<MODE>(a0, x0, y0, sc, bi, d0);
-      if (MODE == 2) store8(dz + o0, d0);
+      if (DZ) store8(dz + o0, d0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         s1[j] += d0[j];
@@ -543,41 +571,42 @@ static Geo apply_geo(int64_t M, int C, const void* fn) {
 void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, float* rmean,
                      float* rvar, const float* gamma, const float* beta, float momentum, float eps,
                      bool relu, float* partial, int P, float* save_mean, float* save_invstd,
-                     float* scale, float* bias, hipStream_t st) {
+                     float* scale, float* bias, hipStream_t st, void* mask) {
   Geo gr = reduce_geo(M, C, P, (const void*)&stats_kernel);
   dim3 grr = grid_of(gr);
   hipLaunchKernelGGL(stats_kernel, grr, dim3(kBlock), 0, st, (const __bf16*)x, rmean, partial, gr);
   hipLaunchKernelGGL(finalize_fwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
                      partial, (int)grr.x, M, C, rmean, rvar, gamma, beta, momentum, eps, save_mean,
                      save_invstd, scale, bias);
-  if (y) mv_bn_apply(x, res, y, M, C, scale, bias, relu, st);   // y == null: statistics only
+  if (y) mv_bn_apply(x, res, y, M, C, scale, bias, relu, st, mask);   // y == null: statistics only
 }
 
 template <bool RELU, bool RES>
 static void launch_apply(const __bf16* x, const __bf16* r, const float* scale, const float* bias,
-                         __bf16* y, int64_t M, int C, hipStream_t st) {
+                         __bf16* y, int64_t M, int C, hipStream_t st, uint8_t* mask) {
   if (bn_nt()) {
     Geo ga = apply_geo(M, C, (const void*)&apply_kernel<RELU, RES, true>);
     hipLaunchKernelGGL((apply_kernel<RELU, RES, true>), grid_of(ga), dim3(kBlock), 0, st, x, r,
-                       scale, bias, y, ga);
+                       scale, bias, y, ga, mask);
   } else {
     Geo ga = apply_geo(M, C, (const void*)&apply_kernel<RELU, RES, false>);
     hipLaunchKernelGGL((apply_kernel<RELU, RES, false>), grid_of(ga), dim3(kBlock), 0, st, x, r,
-                       scale, bias, y, ga);
+                       scale, bias, y, ga, mask);
   }
 }
 
 void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
-                 const float* bias, bool relu, hipStream_t st) {
+                 const float* bias, bool relu, hipStream_t st, void* mask) {
+  uint8_t* mk = (uint8_t*)mask;   // add+ReLU only
   const __bf16* xp = (const __bf16*)x;
   const __bf16* rp = (const __bf16*)res;
   __bf16* yp = (__bf16*)y;
   if (res) {
-    if (relu) launch_apply<true, true>(xp, rp, scale, bias, yp, M, C, st);
-    else launch_apply<false, true>(xp, rp, scale, bias, yp, M, C, st);
+    if (relu) launch_apply<true, true>(xp, rp, scale, bias, yp, M, C, st, mk);
+    else launch_apply<false, true>(xp, rp, scale, bias, yp, M, C, st, nullptr);
   } else {
-    if (relu) launch_apply<true, false>(xp, rp, scale, bias, yp, M, C, st);
-    else launch_apply<false, false>(xp, rp, scale, bias, yp, M, C, st);
+    if (relu) launch_apply<true, false>(xp, rp, scale, bias, yp, M, C, st, nullptr);
+    else launch_apply<false, false>(xp, rp, scale, bias, yp, M, C, st, nullptr);
   }
 }
 
@@ -629,7 +658,8 @@ void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const v
   switch (mode) {
     case 0: pa = launch_bwd_reduce<0>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, dy2_stride, H, W, st); break;
     case 1: pa = launch_bwd_reduce<1>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, dy2_stride, H, W, st); break;
-    default: pa = launch_bwd_reduce<2>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, dy2_stride, H, W, st); break;
+    case 2: pa = launch_bwd_reduce<2>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, dy2_stride, H, W, st); break;
+    default: pa = launch_bwd_reduce<3>(dyp, dy2p, xp, yp, save_mean, scale, bias, dzp, partial, P, M, C, dy2_stride, H, W, st); break;
   }
   hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
                      partial, pa, M, C, save_mean, save_invstd, gamma, dgamma, dbeta, ca, cb, cc);

@@ -17,6 +17,10 @@ import torch.nn.functional as F
 
 from . import kernels as K
 
+# MIVOD_BN_MASK=0: add+ReLU backward re-reads the bf16 output (mode 2) instead of the
+# forward's bitmask (mode 3) -- A/B switch
+_BN_MASK = os.environ.get("MIVOD_BN_MASK", "1") != "0"
+
 
 def _fusable(x: torch.Tensor, weight) -> bool:
     if os.environ.get("MIVOD_FUSED_BN", "1") == "0":     # eager reference path (tests)
@@ -144,13 +148,20 @@ class _BNActTrain(torch.autograd.Function):
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual,
                 slot):
         nat = K.native()
-        y, vec = nat.bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps, relu,
-                                  residual)
         mode = 2 if (relu and residual is not None) else (1 if relu else 0)
+        if mode == 2 and _BN_MASK:
+            # add+ReLU: backward reads a 1-bit-per-channel mask of y > 0 (mode 3), not y
+            y, vec, keep = nat.bn_fwd_train_mask(x, weight, bias, running_mean, running_var,
+                                                 momentum, eps, residual)
+            mode = 3
+        else:
+            y, vec = nat.bn_fwd_train(x, weight, bias, running_mean, running_var, momentum, eps,
+                                      relu, residual)
+            keep = y if mode == 2 else None
         ctx.mode = mode
         ctx.has_res = residual is not None
         ctx.slot = slot
-        ctx.save_for_backward(x, y if mode == 2 else None, vec, weight)
+        ctx.save_for_backward(x, keep, vec, weight)
         return y
 
     @staticmethod
@@ -160,13 +171,13 @@ class _BNActTrain(torch.autograd.Function):
         need_affine = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
         dy2, s2 = None, 1
         if ctx.slot is not None:
-            dy2, s2 = ctx.slot.take_strided() if ctx.mode == 2 else (ctx.slot.take(), 1)
-        if dy2 is not None and ctx.mode != 2:
+            dy2, s2 = ctx.slot.take_strided() if ctx.mode >= 2 else (ctx.slot.take(), 1)
+        if dy2 is not None and ctx.mode < 2:
             dy, dy2 = dy + dy2, None
         dx, dg, db, dz = K.native().bn_bwd(ctx.mode, dy, x, y, vec, weight, need_affine, dy2, s2)
         dres = None
         if ctx.has_res and ctx.needs_input_grad[8]:
-            dres = dz if ctx.mode == 2 else dy
+            dres = dz if ctx.mode >= 2 else dy
         return (dx if ctx.needs_input_grad[0] else None,
                 dg if ctx.needs_input_grad[1] else None,
                 db if ctx.needs_input_grad[2] else None,

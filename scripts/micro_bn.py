@@ -38,6 +38,8 @@ def run(reps):
             y2, vec2 = nat.bn_fwd_train(x, g, b, rm, rv, 0.1, 1e-5, True, res)
             nat.bn_bwd(1, dy, x, None, vec, g, True, None, 1)
             nat.bn_bwd(2, dy, x, y2, vec2, g, True, dy2, 1)
+            y3, vec3, mk = nat.bn_fwd_train_mask(x, g, b, rm, rv, 0.1, 1e-5, res)
+            nat.bn_bwd(3, dy, x, mk, vec3, g, True, dy2, 1)
         torch.cuda.synchronize()
         time.sleep(0.05)
         del x, res, dy, dy2, y1, y2

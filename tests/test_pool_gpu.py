@@ -178,3 +178,31 @@ def test_bn_bwd_strided_second_gradient(cuda):
         ref = nat.bn_bwd(2, dy, x, y, vec, g, True, _cl(full), 1)
         for a, c in zip(got, ref):
             assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("shape,stride", [((8, 64, 14, 14), 1), ((3, 256, 7, 7), 1),
+                                          ((2, 64, 14, 14), 2), ((1, 8, 3, 5), 1)])
+def test_bn_bwd_bitmask_mode_equals_saved_output_mode(cuda, shape, stride):
+    """Mode 3 (the add+ReLU forward's [M, C/8] bitmask of y > 0) == mode 2 (re-reading
+    the bf16 output y), bitwise, with and without a (strided) second gradient stream."""
+    nat = K.native()
+    torch.manual_seed(4)
+    N, C, H, W = shape
+    x = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16))
+    r = _cl(torch.randn(shape, device=cuda).to(torch.bfloat16))
+    g = torch.rand(C, device=cuda) + 0.5
+    b = torch.randn(C, device=cuda) * 0.1
+    y, vec = nat.bn_fwd_train(x, g, b, None, None, 0.1, 1e-5, True, r)
+    y3, vec3, mask = nat.bn_fwd_train_mask(x, g, b, None, None, 0.1, 1e-5, r)
+    assert torch.equal(y, y3) and torch.equal(vec, vec3)
+    M = N * H * W
+    bits = (y.permute(0, 2, 3, 1).reshape(M, C // 8, 8) > 0).to(torch.int32)
+    ref_mask = (bits << torch.arange(8, device=cuda, dtype=torch.int32)).sum(-1).to(torch.uint8)
+    assert mask.shape == (M, C // 8) and torch.equal(mask, ref_mask)
+    dy = _cl(torch.randn_like(x))
+    Ho, Wo = (H + stride - 1) // stride, (W + stride - 1) // stride
+    for dy2 in (None, _cl(torch.randn(N, C, Ho, Wo, device=cuda).to(torch.bfloat16))):
+        got = nat.bn_bwd(3, dy, x, mask, vec, g, True, dy2, stride)
+        ref = nat.bn_bwd(2, dy, x, y, vec, g, True, dy2, stride)
+        for a, c in zip(got, ref):
+            assert torch.equal(a, c)
