@@ -88,6 +88,9 @@ __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
 }
 
 // ---------------------------------------------------------------- forward
+// U rows in flight per lane per iteration (16-byte loads); U = 8 by default (more
+// bytes in flight for this read-only pass), MIVOD_BN_STATS_U=4 selects the old shape
+template <int U>
 __global__ __launch_bounds__(kBlock) void stats_kernel(const __bf16* __restrict__ x,
                                                         const float* __restrict__ shift,
                                                         float* __restrict__ partial, Geo g) {
@@ -102,17 +105,21 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(const __bf16* __restrict_
   if (valid) {
     if (shift) load8f(shift + c, sh);
     int64_t r = r0 + tr;
-    for (; r + 3 * g.RPI < r1; r += 4 * g.RPI) {
-      float v0[8], v1[8], v2[8], v3[8];
-      load8(x + r * g.C + c, v0);
-      load8(x + (r + g.RPI) * g.C + c, v1);
-      load8(x + (r + 2 * g.RPI) * g.C + c, v2);
-      load8(x + (r + 3 * g.RPI) * g.C + c, v3);
+    for (; r + (U - 1) * g.RPI < r1; r += U * g.RPI) {
+      float v[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load8(x + (r + u * g.RPI) * g.C + c, v[u]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float a = v0[j] - sh[j], b = v1[j] - sh[j], cc = v2[j] - sh[j], d = v3[j] - sh[j];
-        s1[j] += (a + b) + (cc + d);
-        s2[j] += (a * a + b * b) + (cc * cc + d * d);
+        float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float a = v[u][j] - sh[j];
+          a1 += a;
+          a2 += a * a;
+        }
+        s1[j] += a1;
+        s2[j] += a2;
       }
     }
     for (; r < r1; r += g.RPI) {
@@ -572,9 +579,20 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
                      float* rvar, const float* gamma, const float* beta, float momentum, float eps,
                      bool relu, float* partial, int P, float* save_mean, float* save_invstd,
                      float* scale, float* bias, hipStream_t st, void* mask) {
-  Geo gr = reduce_geo(M, C, P, (const void*)&stats_kernel);
-  dim3 grr = grid_of(gr);
-  hipLaunchKernelGGL(stats_kernel, grr, dim3(kBlock), 0, st, (const __bf16*)x, rmean, partial, gr);
+  static const bool u4 = [] {
+    const char* e = std::getenv("MIVOD_BN_STATS_U");
+    return e && e[0] == '4';
+  }();
+  dim3 grr;
+  if (u4) {
+    Geo gr = reduce_geo(M, C, P, (const void*)&stats_kernel<4>);
+    grr = grid_of(gr);
+    hipLaunchKernelGGL(stats_kernel<4>, grr, dim3(kBlock), 0, st, (const __bf16*)x, rmean, partial, gr);
+  } else {
+    Geo gr = reduce_geo(M, C, P, (const void*)&stats_kernel<8>);
+    grr = grid_of(gr);
+    hipLaunchKernelGGL(stats_kernel<8>, grr, dim3(kBlock), 0, st, (const __bf16*)x, rmean, partial, gr);
+  }
   hipLaunchKernelGGL(finalize_fwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
                      partial, (int)grr.x, M, C, rmean, rvar, gamma, beta, momentum, eps, save_mean,
                      save_invstd, scale, bias);
