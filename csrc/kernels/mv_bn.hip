@@ -82,15 +82,22 @@ __device__ __forceinline__ void ld_dy2(const __bf16* dy2, int64_t r, int c, int 
   ldlast<NT>(dy2 + ro * C + c, v);
 }
 
+// First read of a tensor a later pass reads again (statistics / reduce passes):
+// non-temporal when RNT (the default, see bn_rnt)
+template <bool RNT>
+__device__ __forceinline__ void ldfirst(const __bf16* p, float (&v)[8]) {
+  if (RNT) load8_nt(p, v);
+  else load8(p, v);
+}
+
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = p[j];
 }
 
 // ---------------------------------------------------------------- forward
-// U rows in flight per lane per iteration (16-byte loads); U = 8 by default (more
-// bytes in flight for this read-only pass), MIVOD_BN_STATS_U=4 selects the old shape
-template <int U>
+// U rows in flight per lane per iteration (16-byte loads)
+template <int U, bool RNT = false>
 __global__ __launch_bounds__(kBlock) void stats_kernel(const __bf16* __restrict__ x,
                                                         const float* __restrict__ shift,
                                                         float* __restrict__ partial, Geo g) {
@@ -108,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(const __bf16* __restrict_
     for (; r + (U - 1) * g.RPI < r1; r += U * g.RPI) {
       float v[U][8];
 #pragma unroll
-      for (int u = 0; u < U; ++u) load8(x + (r + u * g.RPI) * g.C + c, v[u]);
+      for (int u = 0; u < U; ++u) ldfirst<RNT>(x + (r + u * g.RPI) * g.C + c, v[u]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float a1 = 0.f, a2 = 0.f;
@@ -124,7 +131,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(const __bf16* __restrict_
     }
     for (; r < r1; r += g.RPI) {
       float v0[8];
-      load8(x + r * g.C + c, v0);
+      ldfirst<RNT>(x + r * g.C + c, v0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float a = v0[j] - sh[j];
@@ -235,7 +242,8 @@ __device__ __forceinline__ uint8_t relu_bits(const float (&v)[8]) {
   return (uint8_t)m;
 }
 
-template <bool RELU, bool RES, bool NT = true>
+// U rows in flight per lane per iteration (U = 2 by default; MIVOD_BN_APPLY_U=4)
+template <bool RELU, bool RES, bool NT = true, int U = 4>
 __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict__ x,
                                                         const __bf16* __restrict__ res,
                                                         const float* __restrict__ scale,
@@ -253,26 +261,25 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict_
   const int64_t r0 = (int64_t)blockIdx.x * g.RB;
   const int64_t r1 = (r0 + g.RB < g.M) ? r0 + g.RB : g.M;
   int64_t r = r0 + tr;
-  for (; r + g.RPI < r1; r += 2 * g.RPI) {
-    float v0[8], v1[8], q0[8], q1[8];
-    const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
-    ldlast<NT>(x + o0, v0);
-    ldlast<NT>(x + o1, v1);
-    if (RES) { ldlast<NT>(res + o0, q0); ldlast<NT>(res + o1, q1); }
+  for (; r + (U - 1) * g.RPI < r1; r += U * g.RPI) {
+    float v[U][8], q[U][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float a = __builtin_fmaf(v0[j], sc[j], bi[j]);
-      float b = __builtin_fmaf(v1[j], sc[j], bi[j]);
-      if (RES) { a += q0[j]; b += q1[j]; }
-      if (RELU) { a = fmaxf(a, 0.f); b = fmaxf(b, 0.f); }
-      v0[j] = a;
-      v1[j] = b;
+    for (int u = 0; u < U; ++u) ldlast<NT>(x + (r + u * g.RPI) * g.C + c, v[u]);
+    if (RES) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) ldlast<NT>(res + (r + u * g.RPI) * g.C + c, q[u]);
     }
-    store8(y + o0, v0);
-    store8(y + o1, v1);
-    if (RELU && RES && mask) {
-      mask[r * C8 + c / kVec] = relu_bits(v0);
-      mask[(r + g.RPI) * C8 + c / kVec] = relu_bits(v1);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = __builtin_fmaf(v[u][j], sc[j], bi[j]);
+        if (RES) a += q[u][j];
+        if (RELU) a = fmaxf(a, 0.f);
+        v[u][j] = a;
+      }
+      store8(y + (r + u * g.RPI) * g.C + c, v[u]);
+      if (RELU && RES && mask) mask[(r + u * g.RPI) * C8 + c / kVec] = relu_bits(v[u]);
     }
   }
   for (; r < r1; r += g.RPI) {
@@ -315,7 +322,7 @@ __device__ __forceinline__ void masked(const float (&dy)[8], const float (&x)[8]
 
 // last-use reads (dy2, the saved output y, and dy in MODE 2 where the dx pass reads dz)
 // are non-temporal
-template <int MODE, bool NT = true>
+template <int MODE, bool NT = true, bool RNT = false>
 __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
     const __bf16* __restrict__ dy, const __bf16* __restrict__ dy2, const __bf16* __restrict__ x,
     const __bf16* __restrict__ y,
@@ -340,8 +347,8 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
     for (; r + g.RPI < r1; r += 2 * g.RPI) {
       float a0[8], a1[8], x0[8], x1[8], y0[8], y1[8], d0[8], d1[8];
       const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
-      if (DZ) ldlast<NT>(dy + o0, a0); else load8(dy + o0, a0);
-      if (DZ) ldlast<NT>(dy + o1, a1); else load8(dy + o1, a1);
+      if (DZ) ldlast<NT>(dy + o0, a0); else ldfirst<RNT>(dy + o0, a0);
+      if (DZ) ldlast<NT>(dy + o1, a1); else ldfirst<RNT>(dy + o1, a1);
       if (dy2) {   // second gradient stream of a tapped output (uniform branch)
         float b0[8], b1[8];
         ld_dy2<NT>(dy2, r, c, g.C, ds, H, W, b0);
@@ -349,8 +356,8 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) { a0[j] += b0[j]; a1[j] += b1[j]; }
       }
-      load8(x + o0, x0);
-      load8(x + o1, x1);
+      ldfirst<RNT>(x + o0, x0);
+      ldfirst<RNT>(x + o1, x1);
       if (MODE == 2) { ldlast<NT>(y + o0, y0); ldlast<NT>(y + o1, y1); }
       if (MODE == 3) {
         y0[0] = __uint_as_float((uint32_t)mk[r * C8 + c / kVec]);
@@ -368,14 +375,14 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
     for (; r < r1; r += g.RPI) {
       float a0[8], x0[8], y0[8], d0[8];
       const int64_t o0 = r * g.C + c;
-      if (DZ) ldlast<NT>(dy + o0, a0); else load8(dy + o0, a0);
+      if (DZ) ldlast<NT>(dy + o0, a0); else ldfirst<RNT>(dy + o0, a0);
       if (dy2) {
         float b0[8];
         ld_dy2<NT>(dy2, r, c, g.C, ds, H, W, b0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) a0[j] += b0[j];
       }
-      load8(x + o0, x0);
+      ldfirst<RNT>(x + o0, x0);
       if (MODE == 2) ldlast<NT>(y + o0, y0);
       if (MODE == 3) y0[0] = __uint_as_float((uint32_t)mk[r * C8 + c / kVec]);
       masked<MODE>(a0, x0, y0, sc, bi, d0);
@@ -424,7 +431,7 @@ __global__ __launch_bounds__(kBlock) void finalize_bwd_kernel(
   cc[ch] = -a * sdz * inv_m - b * mean[ch];
 }
 
-template <int MODE, bool NT = true>
+template <int MODE, bool NT = true, int U = 4>
 __global__ __launch_bounds__(kBlock) void bwd_dx_kernel(
     const __bf16* __restrict__ d_in, const __bf16* __restrict__ x,
     const float* __restrict__ scale, const float* __restrict__ bias, const float* __restrict__ ca,
@@ -441,25 +448,22 @@ __global__ __launch_bounds__(kBlock) void bwd_dx_kernel(
   const int64_t r0 = (int64_t)blockIdx.x * g.RB;
   const int64_t r1 = (r0 + g.RB < g.M) ? r0 + g.RB : g.M;
   int64_t r = r0 + tr;
-  for (; r + g.RPI < r1; r += 2 * g.RPI) {
-    float d0[8], d1[8], x0[8], x1[8];
-    const int64_t o0 = r * g.C + c, o1 = (r + g.RPI) * g.C + c;
-    ldlast<NT>(d_in + o0, d0);
-    ldlast<NT>(d_in + o1, d1);
-    ldlast<NT>(x + o0, x0);
-    ldlast<NT>(x + o1, x1);
+  for (; r + (U - 1) * g.RPI < r1; r += U * g.RPI) {
+    float d[U][8], xv[U][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float e0 = d0[j], e1 = d1[j];
-      if (MODE == 1) {
-        e0 = __builtin_fmaf(x0[j], sc[j], bi[j]) > 0.f ? e0 : 0.f;
-        e1 = __builtin_fmaf(x1[j], sc[j], bi[j]) > 0.f ? e1 : 0.f;
+    for (int u = 0; u < U; ++u) ldlast<NT>(d_in + (r + u * g.RPI) * g.C + c, d[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) ldlast<NT>(x + (r + u * g.RPI) * g.C + c, xv[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float e = d[u][j];
+        if (MODE == 1) e = __builtin_fmaf(xv[u][j], sc[j], bi[j]) > 0.f ? e : 0.f;
+        d[u][j] = a[j] * e + (b[j] * xv[u][j] + k[j]);
       }
-      d0[j] = a[j] * e0 + (b[j] * x0[j] + k[j]);
-      d1[j] = a[j] * e1 + (b[j] * x1[j] + k[j]);
+      store8(dx + (r + u * g.RPI) * g.C + c, d[u]);
     }
-    store8(dx + o0, d0);
-    store8(dx + o1, d1);
   }
   for (; r < r1; r += g.RPI) {
     float d0[8], x0[8];
@@ -567,6 +571,18 @@ static bool bn_nt() {
   return on;
 }
 
+// Non-temporal loads in the statistics / reduce passes too (MIVOD_BN_RNT=0: default
+// policy).  scripts/micro_bn.py, bs512 shapes: stats 202 -> 125 us and reduce(ReLU)
+// 335 -> 257 us at [1.6M, 256]; the following apply / dx pass loses ~50 us of that
+// (it no longer finds lines the reduce pass left behind), net ~4% per BN layer.
+static bool bn_rnt() {
+  static const bool on = [] {
+    const char* e = std::getenv("MIVOD_BN_RNT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static Geo reduce_geo(int64_t M, int C, int P, const void* fn) {
   return round_geo(M, C, fn, 64, P);
 }
@@ -579,15 +595,12 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
                      float* rvar, const float* gamma, const float* beta, float momentum, float eps,
                      bool relu, float* partial, int P, float* save_mean, float* save_invstd,
                      float* scale, float* bias, hipStream_t st, void* mask) {
-  static const bool u4 = [] {
-    const char* e = std::getenv("MIVOD_BN_STATS_U");
-    return e && e[0] == '4';
-  }();
   dim3 grr;
-  if (u4) {
-    Geo gr = reduce_geo(M, C, P, (const void*)&stats_kernel<4>);
+  if (bn_rnt()) {
+    Geo gr = reduce_geo(M, C, P, (const void*)&stats_kernel<8, true>);
     grr = grid_of(gr);
-    hipLaunchKernelGGL(stats_kernel<4>, grr, dim3(kBlock), 0, st, (const __bf16*)x, rmean, partial, gr);
+    hipLaunchKernelGGL((stats_kernel<8, true>), grr, dim3(kBlock), 0, st, (const __bf16*)x, rmean,
+                       partial, gr);
   } else {
     Geo gr = reduce_geo(M, C, P, (const void*)&stats_kernel<8>);
     grr = grid_of(gr);
@@ -599,17 +612,33 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
   if (y) mv_bn_apply(x, res, y, M, C, scale, bias, relu, st, mask);   // y == null: statistics only
 }
 
+// apply / dx passes: 2 rows in flight per lane; MIVOD_BN_APPLY_U=4 selects 4 (measured
+// equal on the bs512 shapes, scripts/micro_bn.py)
+static bool apply_u2() {
+  static const bool on = [] {
+    const char* e = std::getenv("MIVOD_BN_APPLY_U");
+    return !(e && e[0] == '4');
+  }();
+  return on;
+}
+
+template <bool RELU, bool RES, bool NT, int U>
+static void launch_apply_u(const __bf16* x, const __bf16* r, const float* scale,
+                           const float* bias, __bf16* y, int64_t M, int C, hipStream_t st,
+                           uint8_t* mask) {
+  Geo ga = apply_geo(M, C, (const void*)&apply_kernel<RELU, RES, NT, U>);
+  hipLaunchKernelGGL((apply_kernel<RELU, RES, NT, U>), grid_of(ga), dim3(kBlock), 0, st, x, r,
+                     scale, bias, y, ga, mask);
+}
+
 template <bool RELU, bool RES>
 static void launch_apply(const __bf16* x, const __bf16* r, const float* scale, const float* bias,
                          __bf16* y, int64_t M, int C, hipStream_t st, uint8_t* mask) {
   if (bn_nt()) {
-    Geo ga = apply_geo(M, C, (const void*)&apply_kernel<RELU, RES, true>);
-    hipLaunchKernelGGL((apply_kernel<RELU, RES, true>), grid_of(ga), dim3(kBlock), 0, st, x, r,
-                       scale, bias, y, ga, mask);
+    if (apply_u2()) launch_apply_u<RELU, RES, true, 2>(x, r, scale, bias, y, M, C, st, mask);
+    else launch_apply_u<RELU, RES, true, 4>(x, r, scale, bias, y, M, C, st, mask);
   } else {
-    Geo ga = apply_geo(M, C, (const void*)&apply_kernel<RELU, RES, false>);
-    hipLaunchKernelGGL((apply_kernel<RELU, RES, false>), grid_of(ga), dim3(kBlock), 0, st, x, r,
-                       scale, bias, y, ga, mask);
+    launch_apply_u<RELU, RES, false, 2>(x, r, scale, bias, y, M, C, st, mask);
   }
 }
 
@@ -633,6 +662,13 @@ static int launch_bwd_reduce(const __bf16* dy, const __bf16* dy2, const __bf16* 
                              const __bf16* y, const float* mean, const float* scale,
                              const float* bias, __bf16* dz, float* partial, int P, int64_t M,
                              int C, int ds, int H, int W, hipStream_t st) {
+  if (bn_nt() && bn_rnt()) {
+    Geo gr = reduce_geo(M, C, P, (const void*)&bwd_reduce_kernel<MODE, true, true>);
+    dim3 grr = grid_of(gr);
+    hipLaunchKernelGGL((bwd_reduce_kernel<MODE, true, true>), grr, dim3(kBlock), 0, st, dy, dy2, x,
+                       y, mean, scale, bias, dz, partial, gr, ds, H, W);
+    return (int)grr.x;
+  }
   if (bn_nt()) {
     Geo gr = reduce_geo(M, C, P, (const void*)&bwd_reduce_kernel<MODE, true>);
     dim3 grr = grid_of(gr);
@@ -647,18 +683,24 @@ static int launch_bwd_reduce(const __bf16* dy, const __bf16* dy2, const __bf16* 
   return (int)grr.x;
 }
 
+template <int MODE, bool NT, int U>
+static void launch_bwd_dx_u(const __bf16* d, const __bf16* x, const float* scale,
+                            const float* bias, const float* ca, const float* cb, const float* cc,
+                            __bf16* dx, int64_t M, int C, hipStream_t st) {
+  Geo ga = apply_geo(M, C, (const void*)&bwd_dx_kernel<MODE, NT, U>);
+  hipLaunchKernelGGL((bwd_dx_kernel<MODE, NT, U>), grid_of(ga), dim3(kBlock), 0, st, d, x, scale,
+                     bias, ca, cb, cc, dx, ga);
+}
+
 template <int MODE>
 static void launch_bwd_dx(const __bf16* d, const __bf16* x, const float* scale, const float* bias,
                           const float* ca, const float* cb, const float* cc, __bf16* dx, int64_t M,
                           int C, hipStream_t st) {
   if (bn_nt()) {
-    Geo ga = apply_geo(M, C, (const void*)&bwd_dx_kernel<MODE, true>);
-    hipLaunchKernelGGL((bwd_dx_kernel<MODE, true>), grid_of(ga), dim3(kBlock), 0, st, d, x, scale,
-                       bias, ca, cb, cc, dx, ga);
+    if (apply_u2()) launch_bwd_dx_u<MODE, true, 2>(d, x, scale, bias, ca, cb, cc, dx, M, C, st);
+    else launch_bwd_dx_u<MODE, true, 4>(d, x, scale, bias, ca, cb, cc, dx, M, C, st);
   } else {
-    Geo ga = apply_geo(M, C, (const void*)&bwd_dx_kernel<MODE, false>);
-    hipLaunchKernelGGL((bwd_dx_kernel<MODE, false>), grid_of(ga), dim3(kBlock), 0, st, d, x,
-                       scale, bias, ca, cb, cc, dx, ga);
+    launch_bwd_dx_u<MODE, false, 2>(d, x, scale, bias, ca, cb, cc, dx, M, C, st);
   }
 }
 

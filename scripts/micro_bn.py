@@ -16,7 +16,8 @@ SHAPES = [(6422528, 64), (1605632, 64), (1605632, 256), (401408, 128), (401408, 
 # bytes per element each kernel must move (bf16 = 2 B)
 BYTES = {"stats_kernel": 2, "apply_kernelILb1ELb0": 4, "apply_kernelILb1ELb1": 6,
          "apply_kernelILb0ELb0": 4, "bwd_reduce_kernelILi1": 4, "bwd_reduce_kernelILi2": 10,
-         "bwd_reduce_kernelILi0": 4, "bwd_dx_kernelILi1": 6, "bwd_dx_kernelILi0": 6}
+         "bwd_reduce_kernelILi0": 4, "bwd_reduce_kernelILi3": 8.125,
+         "bwd_dx_kernelILi1": 6, "bwd_dx_kernelILi0": 6}
 
 
 def run(reps):
