@@ -83,7 +83,9 @@ __device__ __forceinline__ void ld_dy2(const __bf16* dy2, int64_t r, int c, int 
 }
 
 // First read of a tensor a later pass reads again (statistics / reduce passes):
-// non-temporal when RNT (the default, see bn_rnt)
+// non-temporal when RNT (the default, see bn_rnt).  The add+ReLU reduce (DZ) keeps x
+// default-policy: its reduce time is unchanged either way, and the dx pass that follows
+// runs ~8% faster on the lines it leaves (micro_bn: 491 -> 454 us at [6.4M, 64])
 template <bool RNT>
 __device__ __forceinline__ void ldfirst(const __bf16* p, float (&v)[8]) {
   if (RNT) load8_nt(p, v);
@@ -356,8 +358,8 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) { a0[j] += b0[j]; a1[j] += b1[j]; }
       }
-      ldfirst<RNT>(x + o0, x0);
-      ldfirst<RNT>(x + o1, x1);
+      ldfirst<RNT && !DZ>(x + o0, x0);
+      ldfirst<RNT && !DZ>(x + o1, x1);
       if (MODE == 2) { ldlast<NT>(y + o0, y0); ldlast<NT>(y + o1, y1); }
       if (MODE == 3) {
         y0[0] = __uint_as_float((uint32_t)mk[r * C8 + c / kVec]);
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(kBlock) void bwd_reduce_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) a0[j] += b0[j];
       }
-      ldfirst<RNT>(x + o0, x0);
+      ldfirst<RNT && !DZ>(x + o0, x0);
       if (MODE == 2) ldlast<NT>(y + o0, y0);
       if (MODE == 3) y0[0] = __uint_as_float((uint32_t)mk[r * C8 + c / kVec]);
       masked<MODE>(a0, x0, y0, sc, bi, d0);
