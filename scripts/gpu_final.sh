@@ -11,5 +11,5 @@ for i in 1 2 3; do timeout -k 10 300 python bench.py > gpurun_out/final_bench$i.
 rm -rf /tmp/prof_final
 timeout -k 10 600 rocprofv3 --kernel-trace -d /tmp/prof_final -o run --output-format csv -- python bench.py --steps 6 --warmup 3 > gpurun_out/final_prof.log 2>&1 || exit 1
 f=$(find /tmp/prof_final -name "*kernel_trace.csv" | head -1)
-python scripts/prof_summary.py "$f" --steps 5 --title "ResNet-50 bf16 bs1024 1xMI355X — bench.py default (round-1 final)" > gpurun_out/summary_final.md 2>&1
+python scripts/prof_summary.py "$f" --steps 5 --title "ResNet-50 bf16 bs2048 1xMI355X — bench.py default (round-1 final)" > gpurun_out/summary_final.md 2>&1
 head -8 gpurun_out/summary_final.md
