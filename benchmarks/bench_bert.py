@@ -19,27 +19,44 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 # GEMM selection: PyTorch TunableOp replays a table of the fastest hipBLASLt / rocBLAS
 # solution per BERT-Large GEMM shape, tuned once on MI355X and shipped in .tunableop/
-# (scripts/gpu_bert_sweep.sh regenerates it).  bs256: 2672 -> 2809 seq/s.
-_TUNED = os.path.join(ROOT, ".tunableop", "bert_large_bs256_seq128.csv")
-if os.path.exists(_TUNED) and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ:
+# (scripts/gpu_bert_sweep.sh / gpu_bert_bs512.sh regenerate them), one per per-GPU batch.
+# TunableOp reads the table under a device-ordinal-suffixed name, so the shipped table is
+# staged into a private directory under both the plain and every ordinal-suffixed name.
+
+
+def _stage_tunableop(batch: int, seq: int) -> None:
+    src = os.path.join(ROOT, ".tunableop", f"bert_large_bs{batch}_seq{seq}.csv")
+    if not os.path.exists(src) or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
+        return
+    import shutil
+    import tempfile
+    d = os.path.join(tempfile.gettempdir(), f"mivod_tunableop_{os.getuid()}")
+    os.makedirs(d, exist_ok=True)
+    base = os.path.join(d, f"bert_large_bs{batch}_seq{seq}")
+    for name in [base + ".csv"] + [f"{base}{i}.csv" for i in range(64)]:
+        part = f"{name}.{os.getpid()}.part"
+        shutil.copyfile(src, part)
+        os.replace(part, name)      # atomic: the ranks of one node share the directory
     os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "1"
     os.environ.setdefault("PYTORCH_TUNABLEOP_TUNING", "0")
-    os.environ.setdefault("PYTORCH_TUNABLEOP_FILENAME", _TUNED)
+    os.environ.setdefault("PYTORCH_TUNABLEOP_FILENAME", base + ".csv")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    # 256 sequences per GPU (32k tokens): BERT-Large GEMMs reach ~1-1.3 PFLOP/s;
-    # bs64 2020 -> bs128 2393 -> bs256 2672 seq/s (1x MI355X, untuned GEMMs)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU sequences")
+    # 512 sequences per GPU (64k tokens): bs64 2020 -> bs128 2393 -> bs256 2672 seq/s
+    # (1x MI355X, untuned GEMMs); bs256 2733 vs bs512 2962 untuned / 3048 tuned (one box)
+    ap.add_argument("--batch", type=int, default=512, help="per-GPU sequences")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--model", default="large", choices=["large", "base", "tiny"])
     ap.add_argument("--compression", default="fp16", choices=["none", "fp16", "bf16"])
     ap.add_argument("--op", default="adasum", choices=["adasum", "average"])
     ap.add_argument("--lr", type=float, default=1e-4)
     args = ap.parse_args()
+    if args.model == "large":
+        _stage_tunableop(args.batch, args.seq)
 
     import torch
 
