@@ -8,11 +8,22 @@ xGMI through mivod's static bucket schedule on the comm stream) and the fused
 SGD-momentum update — on a fixed per-GPU batch (weak scaling).
 
     python bench.py --gpus 1 --steps 30 --warmup 10
+    python bench.py --gpus 8                      # spawns its own 8 ranks
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
         --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 8
 
+``--gpus N`` without a launcher environment (no WORLD_SIZE / HOROVOD_RANK):
+bench.py starts N rank processes itself through mivod's launcher
+(``mivod.run.launcher.launch``, the horovodrun path) BEFORE touching the GPU,
+one per GPU, and exits with their status.  Fewer than N visible GPUs is an
+error unless ``MIVOD_BENCH_SHARE_GPUS=1`` (test rehearsal: ranks share GPUs
+over ``MIVOD_TRANSPORT=gloo-gpu``, since RCCL refuses two ranks on one GPU).
+
 Data: synthetic, generated on the GPU once (uniform images, random labels);
-weights: random init.  Rank 0 prints ONE JSON line.
+weights: random init.  Rank 0 prints ONE JSON line, with a ``comm`` record:
+gradient buckets, bytes per step, collectives per step and the exposed
+communication time (comm-stream work still running after backward's last
+kernel was enqueued, per step).
 """
 from __future__ import annotations
 
@@ -34,11 +45,12 @@ for _d in ("FWD", "BWD", "WRW"):
 _MIO = os.path.join(os.path.dirname(os.path.abspath(__file__)), ".miopen")
 if os.path.isdir(_MIO) and "MIOPEN_USER_DB_PATH" not in os.environ:
     import shutil
-    import tempfile
-    _tmp = os.path.join(tempfile.gettempdir(), f"mivod_miopen_{os.getuid()}")
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from mivod.utils.privdir import private_tmp
+    _tmp = private_tmp("miopen")            # 0700, owner-checked (not a shared /tmp path)
     for sub, var in (("db", "MIOPEN_USER_DB_PATH"), ("cache", "MIOPEN_CUSTOM_CACHE_DIR")):
         dst = os.path.join(_tmp, sub)
-        os.makedirs(dst, exist_ok=True)
+        os.makedirs(dst, mode=0o700, exist_ok=True)
         src = os.path.join(_MIO, sub)
         if os.path.isdir(src):
             for f in os.listdir(src):
@@ -78,26 +90,51 @@ def parse():
 
 def _transport(size: int) -> str:
     from mivod.common import basics
-    if size == 1:
+    st = basics.state()
+    if size == 1 and st.gpu is None:
         return "local"
-    return "rccl" if basics.state().backend == "nccl" else basics.state().backend
+    return st.backend
+
+
+def self_launch(argv, nproc: int, script: str = None) -> int:
+    """Start ``nproc`` ranks of this script (one per GPU) and wait for them.
+    Runs before any GPU call in this process (device_count() does not
+    initialise the GPU), so no process that touched the GPU is ever replaced."""
+    import torch
+    from mivod.run.launcher import assign_slots, launch
+    ndev = torch.cuda.device_count()
+    extra = {}
+    if ndev < nproc:
+        if os.environ.get("MIVOD_BENCH_SHARE_GPUS", "0") != "1":
+            print(f"bench.py: --gpus {nproc} but only {ndev} GPU(s) are visible "
+                  "(set MIVOD_BENCH_SHARE_GPUS=1 to rehearse with shared GPUs)", file=sys.stderr)
+            return 2
+        extra["MIVOD_TRANSPORT"] = os.environ.get("MIVOD_TRANSPORT", "gloo-gpu")
+    slots = assign_slots([("localhost", nproc)], nproc)
+    cmd = [sys.executable, script or os.path.abspath(__file__)] + list(argv)
+    return launch(slots, cmd, extra, tag_output=False)
+
+
+def _launched() -> bool:
+    return any(k in os.environ for k in ("WORLD_SIZE", "HOROVOD_RANK", "OMPI_COMM_WORLD_RANK"))
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and not _launched():
+        sys.exit(self_launch(sys.argv[1:], args.gpus))
     import torch
     import torch.nn.functional as F
 
     import mivod.torch as hvd
     from mivod.models.resnet import resnet50, to_mixed_bf16
     from mivod.optim import FusedLARS, FusedSGD
+    from mivod.parallel import collectives as C
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} needs a launcher (torch.distributed.run / "
-                  "mivodrun); running on the ranks provided", file=sys.stderr)
     hvd.init()
+    if hvd.size() != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {hvd.size()} ranks; "
+              "reporting the actual world size", file=sys.stderr)
     rank, size = hvd.rank(), hvd.size()
     dev = hvd.device()
     assert dev.type == "cuda", "bench.py needs a GPU"
@@ -154,29 +191,48 @@ def main():
     torch.cuda.synchronize()
     warm_s = time.perf_counter() - t_w0
 
-    def barrier():
-        if size > 1:
-            import torch.distributed as dist
-            if dist.get_backend() == "nccl":
-                dist.barrier(device_ids=[dev.index])
-            else:                      # MIVOD_TRANSPORT=gloo-gpu rehearsal (ranks share a GPU)
-                dist.barrier()
-        torch.cuda.synchronize()
+    comm_stream = hvd.comm_stream()
+    timing = []                       # (backward enqueued, comm stream drained) per step
 
-    barrier()
+    def timed_step():
+        out = model(images)
+        loss = F.cross_entropy(out.float(), labels)
+        loss.backward()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        opt.step()
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(comm_stream)
+        opt.zero_grad(set_to_none=True)
+        timing.append((e0, e1))
+        return loss
+
+    run = step if args.graph else timed_step
+    stats0 = C.gpu_stats()
+    C.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
-    barrier()
+    C.barrier()
     elapsed = time.perf_counter() - t0
-    if size > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = C.max_over_ranks(elapsed)
+    stats1 = C.gpu_stats()
     ms = elapsed / max(args.steps, 1) * 1000.0
     ips = args.batch * size * args.steps / elapsed
+    plan = opt.bucket_plan()
+    grad_bytes = sum(nb for _, nb, _ in plan)
+    exposed = [max(0.0, a.elapsed_time(b)) for a, b in timing] if timing else []
+    calls = (stats1.get("calls", 0) - stats0.get("calls", 0)) / max(args.steps, 1)
+    comm = {
+        "buckets": len(plan),
+        "grad_bytes_per_step": grad_bytes,
+        "ring_wire_bytes_per_rank_per_step": int(2 * (size - 1) / size * grad_bytes),
+        "collectives_per_step": round(calls, 2),
+        "exposed_comm_ms": round(sum(exposed) / len(exposed), 3) if exposed else None,
+        "exposed_comm_ms_max": round(max(exposed), 3) if exposed else None,
+    }
     if rank == 0:
         print(f"[bench] warmup {args.warmup} steps {warm_s:.1f}s; loss {float(loss.detach()):.4f}; "
               f"{ms:.2f} ms/step; buckets={len(opt.bucket_plan())}; peak HBM "
@@ -206,6 +262,7 @@ def main():
                 "transport": _transport(size),
                 "hip_graph": bool(args.graph),
             },
+            "comm": comm,
         }
         print(json.dumps(rec), flush=True)
     hvd.shutdown()

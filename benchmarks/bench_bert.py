@@ -3,9 +3,10 @@
 with fp16 gradient compression + Adasum through mivod.torch.DistributedOptimizer.
 
     python benchmarks/bench_bert.py --steps 20 --warmup 5
+    python benchmarks/bench_bert.py --gpus 8          # spawns its own 8 ranks
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
-        benchmarks/bench_bert.py
-Prints one JSON line (sequences/sec for the whole job).
+        benchmarks/bench_bert.py --gpus 8
+Prints one JSON line (sequences/sec for the whole job) with a ``comm`` record.
 """
 from __future__ import annotations
 
@@ -29,11 +30,13 @@ def _stage_tunableop(batch: int, seq: int) -> None:
     if not os.path.exists(src) or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
         return
     import shutil
-    import tempfile
-    d = os.path.join(tempfile.gettempdir(), f"mivod_tunableop_{os.getuid()}")
-    os.makedirs(d, exist_ok=True)
+
+    import torch
+    from mivod.utils.privdir import private_tmp
+    d = private_tmp("tunableop")            # 0700, owner-checked
     base = os.path.join(d, f"bert_large_bs{batch}_seq{seq}")
-    for name in [base + ".csv"] + [f"{base}{i}.csv" for i in range(64)]:
+    ndev = max(1, torch.cuda.device_count())
+    for name in [base + ".csv"] + [f"{base}{i}.csv" for i in range(ndev)]:
         part = f"{name}.{os.getpid()}.part"
         shutil.copyfile(src, part)
         os.replace(part, name)      # atomic: the ranks of one node share the directory
@@ -54,7 +57,15 @@ def main():
     ap.add_argument("--compression", default="fp16", choices=["none", "fp16", "bf16"])
     ap.add_argument("--op", default="adasum", choices=["adasum", "average"])
     ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--gpus", type=int, default=1)
     args = ap.parse_args()
+    if args.gpus > 1 and not any(k in os.environ for k in ("WORLD_SIZE", "HOROVOD_RANK")):
+        sys.path.insert(0, ROOT)
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("mivod_bench", os.path.join(ROOT, "bench.py"))
+        mb = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mb)
+        sys.exit(mb.self_launch(sys.argv[1:], args.gpus, script=os.path.abspath(__file__)))
     if args.model == "large":
         _stage_tunableop(args.batch, args.seq)
 
@@ -63,6 +74,8 @@ def main():
     import mivod.torch as hvd
     from mivod.models.bert import BertConfig, BertForPreTraining, synthetic_batch
     from mivod.optim import FusedAdam
+    from mivod.common import basics
+    from mivod.parallel import collectives as C
 
     hvd.init()
     rank, size, dev = hvd.rank(), hvd.size(), hvd.device()
@@ -79,10 +92,20 @@ def main():
     g.manual_seed(100 + rank)
     batch = synthetic_batch(cfg, args.batch, args.seq, dev, generator=g)
 
-    def step():
+    comm_stream = hvd.comm_stream()
+    timing = []
+
+    def step(timed=False):
         loss = model(*batch)
         loss.backward()
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         opt.step()
+        if timed:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(comm_stream)
+            timing.append((e0, e1))
         opt.zero_grad(set_to_none=True)
         return loss
 
@@ -94,26 +117,23 @@ def main():
             print(f"[bert] first step {time.perf_counter() - t0:.1f}s", file=sys.stderr,
                   flush=True)
     torch.cuda.synchronize()
-    if size > 1:
-        if torch.distributed.get_backend() == "nccl":
-            torch.distributed.barrier(device_ids=[dev.index])
-        else:
-            torch.distributed.barrier()
+    stats0 = C.gpu_stats()
+    C.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = step(timed=True)
     torch.cuda.synchronize()
-    if size > 1:
-        if torch.distributed.get_backend() == "nccl":
-            torch.distributed.barrier(device_ids=[dev.index])
-        else:
-            torch.distributed.barrier()
-    el = time.perf_counter() - t0
-    if size > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el = float(t.item())
+    C.barrier()
+    el = C.max_over_ranks(time.perf_counter() - t0)
+    stats1 = C.gpu_stats()
+    plan = opt.bucket_plan()
+    exposed = [max(0.0, a.elapsed_time(b)) for a, b in timing]
+    comm = {"buckets": len(plan), "grad_bytes_per_step": sum(nb for _, nb, _ in plan),
+            "collectives_per_step": round((stats1.get("calls", 0) - stats0.get("calls", 0))
+                                          / max(args.steps, 1), 2),
+            "exposed_comm_ms": round(sum(exposed) / len(exposed), 3) if exposed else None,
+            "guard": opt.guard_stats()}
     if rank == 0:
         print(json.dumps({
             "metric": "sequences/sec (whole node), BERT-Large bf16 pre-training, fp16 compression + Adasum",
@@ -126,7 +146,9 @@ def main():
             "config": {"model": f"BERT-{args.model}", "global_batch": args.batch * size,
                        "seq_len": args.seq, "parallelism": f"dp{size}",
                        "compression": args.compression, "op": args.op,
-                       "optimizer": "mivod FusedAdamW"}}), flush=True)
+                       "optimizer": "mivod FusedAdamW",
+                       "transport": basics.state().backend if size > 1 else "local"},
+            "comm": comm}), flush=True)
     hvd.shutdown()
 
 

@@ -11,10 +11,11 @@ using namespace mvcore;
 
 namespace {
 
-// request tuple: (name, kind, dtype, shape, root, op, device, nbytes)
+// request tuple: (name, kind, dtype, shape, root, op, device, nbytes[, prescale, postscale])
 Request to_request(const py::handle& h) {
   auto t = py::reinterpret_borrow<py::tuple>(h);
-  if (t.size() != 8) throw std::invalid_argument("mivod request must be an 8-tuple");
+  if (t.size() != 8 && t.size() != 10)
+    throw std::invalid_argument("mivod request must be an 8- or 10-tuple");
   Request r;
   r.name = t[0].cast<std::string>();
   r.kind = (uint8_t)t[1].cast<int>();
@@ -24,6 +25,10 @@ Request to_request(const py::handle& h) {
   r.op = t[5].cast<int32_t>();
   r.device = t[6].cast<int32_t>();
   r.nbytes = t[7].cast<int64_t>();
+  if (t.size() == 10) {
+    r.prescale = t[8].cast<double>();
+    r.postscale = t[9].cast<double>();
+  }
   return r;
 }
 
@@ -49,6 +54,8 @@ PYBIND11_MODULE(_mvcore, m) {
       .def("activity", &Timeline::activity, py::call_guard<py::gil_scoped_release>())
       .def("end", &Timeline::end, py::call_guard<py::gil_scoped_release>())
       .def("instant", &Timeline::instant, py::call_guard<py::gil_scoped_release>())
+      .def("complete", &Timeline::complete, py::call_guard<py::gil_scoped_release>())
+      .def("now_us", &Timeline::now_us)
       .def("mark_cycle", &Timeline::mark_cycle, py::call_guard<py::gil_scoped_release>())
       .def("close", &Timeline::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("events_written", &Timeline::events_written);
@@ -76,6 +83,7 @@ PYBIND11_MODULE(_mvcore, m) {
            },
            py::call_guard<py::gil_scoped_release>())
       .def("barrier", &Ring::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("set_timeout", &Ring::set_timeout)
       .def("close", &Ring::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("rank", &Ring::rank)
       .def_property_readonly("size", &Ring::size)
@@ -96,7 +104,8 @@ PYBIND11_MODULE(_mvcore, m) {
       .def_readwrite("stall_check_s", &ControllerConfig::stall_check_s)
       .def_readwrite("stall_shutdown_s", &ControllerConfig::stall_shutdown_s)
       .def_readwrite("stall_check", &ControllerConfig::stall_check)
-      .def_readwrite("connect_timeout_s", &ControllerConfig::connect_timeout_s);
+      .def_readwrite("connect_timeout_s", &ControllerConfig::connect_timeout_s)
+      .def_readwrite("cache_capacity", &ControllerConfig::cache_capacity);
 
   py::class_<Controller>(m, "Controller")
       .def(py::init<const ControllerConfig&>())
@@ -104,19 +113,20 @@ PYBIND11_MODULE(_mvcore, m) {
       .def("connect", &Controller::connect, py::call_guard<py::gil_scoped_release>())
       .def("set_timeline", &Controller::set_timeline)
       .def("negotiate",
-           [](Controller& c, py::list reqs, bool shutdown) {
+           [](Controller& c, py::list reqs, bool shutdown, int64_t position) {
              std::vector<Request> rs;
              rs.reserve(reqs.size());
              for (auto h : reqs) rs.push_back(to_request(h));
              bool all = false;
+             int64_t exec_at = position;
              std::vector<Response> out;
              {
                py::gil_scoped_release nogil;
-               out = c.negotiate(rs, shutdown, &all);
+               out = c.negotiate(rs, shutdown, &all, position, &exec_at);
              }
-             return py::make_tuple(to_py(out), all);
+             return py::make_tuple(to_py(out), all, exec_at);
            },
-           py::arg("requests"), py::arg("shutdown") = false)
+           py::arg("requests"), py::arg("shutdown") = false, py::arg("position") = 0)
       .def("coordinate_for_test",
            [](Controller& c, py::list per_rank) {
              std::vector<std::vector<Request>> pr;
@@ -136,5 +146,7 @@ PYBIND11_MODULE(_mvcore, m) {
            })
       .def_property_readonly("cycles", &Controller::cycles)
       .def_property_readonly("cache_hits", &Controller::cache_hits)
+      .def_property_readonly("bitvector_cycles", &Controller::bitvector_cycles)
+      .def_property_readonly("cache_size", &Controller::cache_size)
       .def("close", &Controller::close, py::call_guard<py::gil_scoped_release>());
 }

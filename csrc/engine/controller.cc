@@ -27,7 +27,8 @@ static std::string shape_str(const std::vector<int64_t>& s) {
 
 static bool same_sig(const Request& a, const Request& b) {
   return a.kind == b.kind && a.dtype == b.dtype && a.shape == b.shape && a.root == b.root &&
-         a.op == b.op && a.device == b.device && a.nbytes == b.nbytes;
+         a.op == b.op && a.device == b.device && a.nbytes == b.nbytes &&
+         a.prescale == b.prescale && a.postscale == b.postscale;
 }
 
 Controller::Controller(const ControllerConfig& cfg) : cfg_(cfg) {
@@ -85,100 +86,173 @@ void Controller::close() {
 }
 
 // ---- response-cache aware request encoding --------------------------------
-// A cached request is sent as (u8 1, u32 id); a new one as (u8 0, full record).
-// Ids are assigned in submission order on the submitting rank and mirrored on
-// the coordinator per rank, so the two sides never need to agree globally.
-std::string Controller::encode_cached(const std::vector<Request>& reqs, bool shutdown) {
+// Message: [u8 shutdown][i64 position][u8 mode]
+//   mode 0: [u32 n] n x ( [u8 0][u32 slot][record]  new, stored in `slot`
+//                       | [u8 1][u32 slot]          cached
+//                       | [u8 2][record] )          uncached (capacity 0)
+//   mode 1: [u32 capacity][capacity/8 bytes: cached-slot bit vector]   (every
+//           request of the cycle was a cache hit and the bit vector is smaller)
+std::string Controller::encode_cached(const std::vector<Request>& reqs, bool shutdown,
+                                      int64_t position) {
   Writer w;
   w.u8(shutdown ? 1 : 0);
+  w.i64(position);
+  const uint32_t cap = (uint32_t)std::max(0, cfg_.cache_capacity);
+  std::vector<uint32_t> hit(reqs.size(), UINT32_MAX);
+  bool all_hit = cap > 0 && !reqs.empty();
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    auto it = cap ? cache_id_.find(reqs[i].name) : cache_id_.end();
+    if (it != cache_id_.end() && same_sig(cache_req_[it->second], reqs[i])) hit[i] = it->second;
+    else all_hit = false;
+  }
+  if (all_hit && (size_t)(cap + 7) / 8 + 4 < reqs.size() * 5) {
+    std::string bits((cap + 7) / 8, '\0');
+    for (uint32_t id : hit) bits[id / 8] |= (char)(1u << (id % 8));
+    w.u8(1);
+    w.u32(cap);
+    w.buf.append(bits);
+    return w.buf;
+  }
+  // sequential encoding, mirrored by the coordinator's sequential decode: a slot
+  // evicted by an earlier request of this message is simply a miss later on
+  w.u8(0);
   w.u32((uint32_t)reqs.size());
-  for (const auto& r : reqs) {
-    auto it = cache_id_.find(r.name);
-    if (it != cache_id_.end() && same_sig(cache_req_[it->second], r)) {
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    const Request& r = reqs[i];
+    auto hit_it = cap ? cache_id_.find(r.name) : cache_id_.end();
+    if (hit_it != cache_id_.end() && same_sig(cache_req_[hit_it->second], r)) {
       w.u8(1);
-      w.u32(it->second);
+      w.u32(hit_it->second);
       continue;
     }
-    w.u8(0);
     std::vector<Request> one{r};
     Writer tmp;
     encode_requests(tmp, one, false);
+    if (cap == 0) {
+      w.u8(2);
+      w.str(tmp.buf);
+      continue;
+    }
+    uint32_t slot;
+    if (hit_it != cache_id_.end()) {
+      slot = hit_it->second;                   // same name, new signature: overwrite
+    } else if (cache_req_.size() < cap) {
+      slot = (uint32_t)cache_req_.size();
+      cache_req_.push_back(r);
+    } else {
+      slot = next_evict_;                      // FIFO eviction
+      next_evict_ = (next_evict_ + 1) % cap;
+      cache_id_.erase(cache_req_[slot].name);
+    }
+    cache_req_[slot] = r;
+    cache_id_[r.name] = slot;
+    w.u8(0);
+    w.u32(slot);
     w.str(tmp.buf);
-    uint32_t id = (uint32_t)cache_req_.size();
-    cache_id_[r.name] = id;
-    cache_req_.push_back(r);
   }
   return w.buf;
 }
 
 std::vector<Request> Controller::decode_cached(const std::string& msg, int from_rank,
-                                               bool* shutdown) {
+                                               bool* shutdown, int64_t* position) {
   Reader rd(msg);
   *shutdown = rd.u8() != 0;
-  uint32_t n = rd.u32();
-  std::vector<Request> out;
-  out.reserve(n);
+  *position = rd.i64();
+  const uint8_t mode = rd.u8();
   auto& pc = peer_cache_[from_rank];
+  std::vector<Request> out;
+  if (mode == 1) {
+    uint32_t cap = rd.u32();
+    std::string bits;
+    for (uint32_t i = 0; i < (cap + 7) / 8; ++i) bits.push_back((char)rd.u8());
+    for (uint32_t id = 0; id < cap; ++id)
+      if (bits[id / 8] & (1u << (id % 8))) {
+        if (id >= pc.size() || pc[id].name.empty())
+          throw std::runtime_error("mivod controller: unknown cache slot");
+        out.push_back(pc[id]);
+        ++cache_hits_;
+      }
+    ++bitvector_cycles_;
+    return out;
+  }
+  uint32_t n = rd.u32();
+  out.reserve(n);
   for (uint32_t i = 0; i < n; ++i) {
-    if (rd.u8() == 1) {
+    uint8_t tag = rd.u8();
+    if (tag == 1) {
       uint32_t id = rd.u32();
-      if (id >= pc.size()) throw std::runtime_error("mivod controller: unknown cache id");
+      if (id >= pc.size() || pc[id].name.empty())
+        throw std::runtime_error("mivod controller: unknown cache slot");
       out.push_back(pc[id]);
       ++cache_hits_;
-    } else {
-      std::string rec = rd.str();
-      Reader r2(rec);
-      bool dummy;
-      auto v = decode_requests(r2, &dummy);
-      if (v.size() != 1) throw std::runtime_error("mivod controller: bad request record");
-      pc.push_back(v[0]);
-      out.push_back(v[0]);
+      continue;
     }
+    uint32_t slot = tag == 0 ? rd.u32() : 0;
+    std::string rec = rd.str();
+    Reader r2(rec);
+    bool dummy;
+    auto v = decode_requests(r2, &dummy);
+    if (v.size() != 1) throw std::runtime_error("mivod controller: bad request record");
+    if (tag == 0) {
+      if (slot >= pc.size()) pc.resize(slot + 1);
+      pc[slot] = v[0];
+    }
+    out.push_back(v[0]);
   }
   return out;
 }
 
 std::vector<Response> Controller::negotiate(const std::vector<Request>& reqs, bool shutdown,
-                                            bool* all_shutdown) {
+                                            bool* all_shutdown, int64_t position,
+                                            int64_t* exec_at) {
   std::lock_guard<std::mutex> g(mu_);
   ++cycles_;
   if (tl_) tl_->mark_cycle();
   *all_shutdown = false;
+  if (exec_at) *exec_at = position;
   if (cfg_.size == 1) {
     std::vector<std::vector<Request>> pr{reqs};
     *all_shutdown = shutdown;
     return coordinate(pr);
   }
   if (cfg_.rank != 0) {
-    send_msg(fd_, encode_cached(reqs, shutdown));
+    send_msg(fd_, encode_cached(reqs, shutdown, position));
     std::string m = recv_msg(fd_);
     Reader rd(m);
     bool sd = false;
     auto resp = decode_responses(rd, &sd);
+    int64_t e = rd.i64();
+    if (exec_at) *exec_at = e;
     *all_shutdown = sd;
     return resp;
   }
   // coordinator: gather (own requests go through the same cache path)
   std::vector<std::vector<Request>> per_rank(cfg_.size);
   int n_shutdown = 0;
+  int64_t emax = position;
   {
-    std::string own = encode_cached(reqs, shutdown);
+    std::string own = encode_cached(reqs, shutdown, position);
     bool sd;
-    per_rank[0] = decode_cached(own, 0, &sd);
+    int64_t pos;
+    per_rank[0] = decode_cached(own, 0, &sd, &pos);
     n_shutdown += sd ? 1 : 0;
   }
   for (int r = 1; r < cfg_.size; ++r) {
     std::string m = recv_msg(peers_[r]);
     bool sd;
-    per_rank[r] = decode_cached(m, r, &sd);
+    int64_t pos;
+    per_rank[r] = decode_cached(m, r, &sd, &pos);
     n_shutdown += sd ? 1 : 0;
+    emax = std::max(emax, pos);
   }
   auto resp = coordinate(per_rank);
   bool done = n_shutdown == cfg_.size;
   Writer w;
   encode_responses(w, resp, done);
+  w.i64(emax);
   for (int r = 1; r < cfg_.size; ++r) send_msg(peers_[r], w.buf);
   *all_shutdown = done;
+  if (exec_at) *exec_at = emax;
   return resp;
 }
 
@@ -215,6 +289,11 @@ std::string Controller::validate(const Entry& e) const {
       o << "Mismatched allreduce reduction ops: " << a.op << " vs " << b.op << ".";
       return o.str();
     }
+    if (a.kind == ALLREDUCE && (a.prescale != b.prescale || a.postscale != b.postscale)) {
+      o << "Mismatched allreduce prescale/postscale factors: (" << a.prescale << ", "
+        << a.postscale << ") vs (" << b.prescale << ", " << b.postscale << ").";
+      return o.str();
+    }
     if (a.kind == BROADCAST && a.root != b.root) {
       o << "Mismatched broadcast root ranks: One rank specified root rank " << a.root
         << ", but another rank specified root rank " << b.root << ".";
@@ -242,7 +321,7 @@ std::string Controller::validate(const Entry& e) const {
 
 std::vector<Response> Controller::fuse(std::vector<Response> ready) const {
   // Horovod-style look-ahead fusion: an allreduce absorbs later compatible
-  // allreduces (same dtype / op / CPU-vs-GPU) while the fused byte count stays
+  // allreduces (same wire dtype / op / pre- and postscale / CPU-vs-GPU) while the fused byte count stays
   // under the threshold.  Adasum (op 2) tensors are never fused across names.
   std::vector<Response> out;
   std::vector<bool> used(ready.size(), false);
@@ -259,6 +338,7 @@ std::vector<Response> Controller::fuse(std::vector<Response> ready) const {
           if (used[j] || ready[j].kind != ALLREDUCE || !ready[j].error.empty()) continue;
           const Request& b = req0(ready[j]);
           if (b.dtype != a.dtype || b.op != a.op || (b.device < 0) != (a.device < 0)) continue;
+          if (b.prescale != a.prescale || b.postscale != a.postscale) continue;
           if (bytes + b.nbytes > cfg_.fusion_threshold) continue;
           bytes += b.nbytes;
           cur.names.push_back(ready[j].names[0]);

@@ -24,6 +24,9 @@ int ring_dtype_size(int dtype);
 
 class Ring {
  public:
+  // per-step I/O timeout once connected (HOROVOD_STALL_SHUTDOWN_TIME_SECONDS):
+  // a dead or stalled peer raises on every surviving rank instead of hanging
+  void set_timeout(double s) { timeout_s_ = s; }
   Ring(int rank, int size, double timeout_s = 300.0);
   ~Ring();
   Ring(const Ring&) = delete;

@@ -46,6 +46,12 @@ void Timeline::end(const std::string& name) { push(Ev{'E', name, "", "", now_us(
 void Timeline::instant(const std::string& name, const std::string& what) {
   push(Ev{'i', name, what, "", now_us()});
 }
+void Timeline::complete(const std::string& name, const std::string& phase, int64_t ts_us,
+                        int64_t dur_us) {
+  Ev e{'X', name, phase, "", ts_us};
+  e.dur = dur_us < 0 ? 0 : dur_us;
+  push(std::move(e));
+}
 void Timeline::mark_cycle() {
   if (mark_cycles_) instant("cycle", "CYCLE_START");
 }
@@ -96,6 +102,10 @@ void Timeline::run() {
           out += b;
           open_[e.name] = false;
         }
+      } else if (e.ph == 'X') {
+        out += "{\"name\": \"" + json_escape(e.phase) + "\", \"ph\": \"X\", \"pid\": " +
+               std::to_string(pid) + ", \"tid\": 2, \"ts\": " + std::to_string(e.ts) +
+               ", \"dur\": " + std::to_string(e.dur) + "},\n";
       } else {
         out += "{\"name\": \"" + json_escape(e.phase) + "\", \"ph\": \"i\", \"s\": \"p\", \"pid\": " +
                std::to_string(pid) + ", \"tid\": 1, \"ts\": " + std::to_string(e.ts) + "},\n";

@@ -23,7 +23,11 @@ class Timeline {
   void activity(const std::string& name, const std::string& phase) { start(name, phase); }
   void end(const std::string& name);
   void instant(const std::string& name, const std::string& what);
+  // complete ("X") event with explicit start / duration in this timeline's clock
+  // (GPU phases of the static gradient schedule, timed by hipEvents)
+  void complete(const std::string& name, const std::string& phase, int64_t ts_us, int64_t dur_us);
   void mark_cycle();
+  int64_t now_us() const;
   void close();
   bool mark_cycles() const { return mark_cycles_; }
   int64_t events_written() const { return written_; }
@@ -33,8 +37,8 @@ class Timeline {
     char ph;
     std::string name, phase, args;
     int64_t ts;
+    int64_t dur = 0;
   };
-  int64_t now_us() const;
   void push(Ev e);
   void run();
   int pid_for(const std::string& name, std::string* meta);

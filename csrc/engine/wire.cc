@@ -29,6 +29,8 @@ void encode_requests(Writer& w, const std::vector<Request>& rs, bool shutdown) {
     w.i32(r.op);
     w.i32(r.device);
     w.i64(r.nbytes);
+    w.f64(r.prescale);
+    w.f64(r.postscale);
   }
 }
 
@@ -47,6 +49,8 @@ std::vector<Request> decode_requests(Reader& rd, bool* shutdown) {
     r.op = rd.i32();
     r.device = rd.i32();
     r.nbytes = rd.i64();
+    r.prescale = rd.f64();
+    r.postscale = rd.f64();
   }
   return rs;
 }

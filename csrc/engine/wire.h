@@ -24,6 +24,8 @@ struct Request {
   int32_t op = 0;
   int32_t device = -1;  // -1 = CPU
   int64_t nbytes = 0;
+  double prescale = 1.0;   // per-rank contribution scale (fused only with equal factors)
+  double postscale = 1.0;
   int32_t rank = 0;     // filled by the coordinator
 };
 
@@ -40,6 +42,7 @@ class Writer {
   void u32(uint32_t v) { buf.append(reinterpret_cast<const char*>(&v), 4); }
   void i32(int32_t v) { buf.append(reinterpret_cast<const char*>(&v), 4); }
   void i64(int64_t v) { buf.append(reinterpret_cast<const char*>(&v), 8); }
+  void f64(double v) { buf.append(reinterpret_cast<const char*>(&v), 8); }
   void str(const std::string& s) { u32((uint32_t)s.size()); buf.append(s); }
 };
 
@@ -50,6 +53,8 @@ class Reader {
   uint32_t u32() { uint32_t v; cp(&v, 4); return v; }
   int32_t i32() { int32_t v; cp(&v, 4); return v; }
   int64_t i64() { int64_t v; cp(&v, 8); return v; }
+  double f64() { double v; cp(&v, 8); return v; }
+  bool done() const { return p_ >= b_.size(); }
   std::string str() { uint32_t n = u32(); need(n); std::string s = b_.substr(p_, n); p_ += n; return s; }
 
  private:

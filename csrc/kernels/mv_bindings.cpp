@@ -120,6 +120,15 @@ void* model_ptr(const c10::optional<at::Tensor>& model, const at::Tensor& g, int
   return model->data_ptr();
 }
 
+// optional device int32 skip flag (fp16-wire overflow guard)
+const int* skip_ptr(const c10::optional<at::Tensor>& skip, const at::Tensor& g) {
+  if (!skip.has_value()) return nullptr;
+  TORCH_CHECK(skip->is_cuda() && skip->scalar_type() == at::kInt && skip->numel() >= 1 &&
+                  skip->device() == g.device(),
+              "skip must be an int32 GPU tensor on the grad's device");
+  return skip->data_ptr<int>();
+}
+
 // optional device hyperparameter block [lr, first, bc1, bc2] (HIP-graph replays)
 const float* dyn_ptr(const c10::optional<at::Tensor>& dyn, const at::Tensor& g) {
   if (!dyn.has_value()) return nullptr;
@@ -131,7 +140,8 @@ const float* dyn_ptr(const c10::optional<at::Tensor>& dyn, const at::Tensor& g) 
 
 void sgd_step(at::Tensor g, at::Tensor w, c10::optional<at::Tensor> mom,
               c10::optional<at::Tensor> model, double lr, double momentum, double dampening,
-              double wd, double gscale, bool nesterov, bool first, c10::optional<at::Tensor> dyn) {
+              double wd, double gscale, bool nesterov, bool first, c10::optional<at::Tensor> dyn,
+              c10::optional<at::Tensor> skip) {
   check_flat(g, "grad");
   check_master(g, w, "master");
   if (mom.has_value()) check_master(g, *mom, "momentum");
@@ -142,13 +152,13 @@ void sgd_step(at::Tensor g, at::Tensor w, c10::optional<at::Tensor> mom,
   mv_launch_sgd(g.data_ptr(), dtype_code(g), w.data_ptr<float>(),
                 mom.has_value() ? mom->data_ptr<float>() : nullptr, mp, md, g.numel(), (float)lr,
                 (float)momentum, (float)dampening, (float)wd, (float)gscale, nesterov, first, dp,
-                cur_stream());
+                skip_ptr(skip, g), cur_stream());
 }
 
 void adam_step(at::Tensor g, at::Tensor w, at::Tensor m, at::Tensor v,
                c10::optional<at::Tensor> model, double lr, double b1, double b2, double eps,
                double wd, double gscale, int64_t step, bool adamw, bool keras_eps,
-               c10::optional<at::Tensor> dyn) {
+               c10::optional<at::Tensor> dyn, c10::optional<at::Tensor> skip) {
   check_flat(g, "grad");
   check_master(g, w, "master");
   check_master(g, m, "exp_avg");
@@ -162,12 +172,12 @@ void adam_step(at::Tensor g, at::Tensor w, at::Tensor m, at::Tensor v,
   mv_launch_adam(g.data_ptr(), dtype_code(g), w.data_ptr<float>(), m.data_ptr<float>(),
                  v.data_ptr<float>(), mp, md, g.numel(), (float)lr, (float)b1, (float)b2,
                  (float)eps, (float)wd, (float)gscale, (float)bc1, (float)bc2, adamw, keras_eps,
-                 dyn_ptr(dyn, g), cur_stream());
+                 dyn_ptr(dyn, g), skip_ptr(skip, g), cur_stream());
 }
 
 void adadelta_step(at::Tensor g, at::Tensor w, at::Tensor sq, at::Tensor acc,
                    c10::optional<at::Tensor> model, double lr, double rho, double eps, double wd,
-                   double gscale, c10::optional<at::Tensor> dyn) {
+                   double gscale, c10::optional<at::Tensor> dyn, c10::optional<at::Tensor> skip) {
   check_flat(g, "grad");
   check_master(g, w, "master");
   check_master(g, sq, "square_avg");
@@ -177,7 +187,7 @@ void adadelta_step(at::Tensor g, at::Tensor w, at::Tensor sq, at::Tensor acc,
   c10::DeviceGuard guard(g.device());
   mv_launch_adadelta(g.data_ptr(), dtype_code(g), w.data_ptr<float>(), sq.data_ptr<float>(),
                      acc.data_ptr<float>(), mp, md, g.numel(), (float)lr, (float)rho, (float)eps,
-                     (float)wd, (float)gscale, dyn_ptr(dyn, g), cur_stream());
+                     (float)wd, (float)gscale, dyn_ptr(dyn, g), skip_ptr(skip, g), cur_stream());
 }
 
 ChunkTable make_table(const at::Tensor& begin, const at::Tensor& len, const at::Tensor& seg,
@@ -206,7 +216,7 @@ void lars_step(at::Tensor g, at::Tensor w, at::Tensor mom, c10::optional<at::Ten
                at::Tensor cbeg, at::Tensor clen, at::Tensor cseg, at::Tensor seg_c0,
                at::Tensor seg_nc, at::Tensor sflag, at::Tensor partial, at::Tensor norms, double lr,
                double momentum, double wd, double eta, double gscale, double eps, bool first,
-               c10::optional<at::Tensor> dyn) {
+               c10::optional<at::Tensor> dyn, c10::optional<at::Tensor> skip) {
   check_flat(g, "grad");
   check_master(g, w, "master");
   check_master(g, mom, "momentum");
@@ -222,21 +232,27 @@ void lars_step(at::Tensor g, at::Tensor w, at::Tensor mom, c10::optional<at::Ten
   mv_launch_lars(g.data_ptr(), dtype_code(g), w.data_ptr<float>(), mom.data_ptr<float>(), mp, md,
                  ct, sflag.data_ptr<int32_t>(), partial.data_ptr<float>(), norms.data_ptr<float>(),
                  (float)lr, (float)momentum, (float)wd, (float)eta, (float)gscale, (float)eps, first,
-                 dyn_ptr(dyn, g), cur_stream());
+                 dyn_ptr(dyn, g), skip_ptr(skip, g), cur_stream());
 }
 
 void seg_dot3(at::Tensor a, at::Tensor b, at::Tensor cbeg, at::Tensor clen, at::Tensor cseg,
               at::Tensor seg_c0, at::Tensor seg_nc, at::Tensor partial, at::Tensor out) {
   check_flat(a, "a");
   check_flat(b, "b");
-  TORCH_CHECK(a.numel() == b.numel() && a.scalar_type() == b.scalar_type(), "seg_dot3: a/b mismatch");
+  TORCH_CHECK(a.numel() == b.numel(), "seg_dot3: a/b numel mismatch");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() || a.scalar_type() == at::kFloat,
+              "seg_dot3: a must match b or be fp32");
   ChunkTable ct = make_table(cbeg, clen, cseg, seg_c0, seg_nc, a.numel());
   TORCH_CHECK(partial.scalar_type() == at::kFloat && partial.numel() >= 3 * ct.nchunks,
               "seg_dot3: partial buffer too small");
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 3 * ct.nseg, "seg_dot3: out too small");
   c10::DeviceGuard guard(a.device());
-  mv_launch_seg_dot3(a.data_ptr(), b.data_ptr(), dtype_code(a), ct, partial.data_ptr<float>(),
-                     out.data_ptr<float>(), cur_stream());
+  if (a.scalar_type() == b.scalar_type())
+    mv_launch_seg_dot3(a.data_ptr(), b.data_ptr(), dtype_code(a), ct, partial.data_ptr<float>(),
+                       out.data_ptr<float>(), cur_stream());
+  else
+    mv_launch_seg_dot3_f(a.data_ptr<float>(), b.data_ptr(), dtype_code(b), ct,
+                         partial.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
 }
 
 void adasum_combine(at::Tensor a, at::Tensor b, at::Tensor cbeg, at::Tensor clen, at::Tensor cseg,
@@ -250,6 +266,20 @@ void adasum_combine(at::Tensor a, at::Tensor b, at::Tensor cbeg, at::Tensor clen
   c10::DeviceGuard guard(a.device());
   mv_launch_adasum_combine(a.data_ptr(), b.data_ptr(), dtype_code(a), ct, dots.data_ptr<float>(),
                            cur_stream());
+}
+
+void adasum_fcombine(at::Tensor f, at::Tensor r, at::Tensor cbeg, at::Tensor clen, at::Tensor cseg,
+                     at::Tensor seg_c0, at::Tensor seg_nc, at::Tensor dots, bool swap) {
+  check_flat(f, "f");
+  check_flat(r, "r");
+  TORCH_CHECK(f.scalar_type() == at::kFloat, "adasum_fcombine: running merge must be fp32");
+  TORCH_CHECK(f.numel() == r.numel(), "adasum_fcombine: f/r numel mismatch");
+  ChunkTable ct = make_table(cbeg, clen, cseg, seg_c0, seg_nc, f.numel());
+  TORCH_CHECK(dots.scalar_type() == at::kFloat && dots.is_contiguous() && dots.numel() >= 3 * ct.nseg,
+              "adasum: dots");
+  c10::DeviceGuard guard(f.device());
+  mv_launch_adasum_fcombine(f.data_ptr<float>(), r.data_ptr(), dtype_code(r), ct,
+                            dots.data_ptr<float>(), swap ? 1 : 0, cur_stream());
 }
 
 // ---------------------------------------------------------------------------
@@ -745,6 +775,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("lars_step", &lars_step, "fused segmented LARS step");
   m.def("seg_dot3", &seg_dot3, "per-segment (a.b, |a|^2, |b|^2)");
   m.def("adasum_combine", &adasum_combine, "per-segment Adasum merge a <- ca*a + cb*b");
+  m.def("adasum_fcombine", &adasum_fcombine,
+        "vector-halving Adasum merge on the fp32 running sum f <- cf*f + cr*r");
   // roctx ranges: rocprofv3 --marker-trace shows mivod's bucket phases (pack,
   // allreduce, fused step) on the same timeline as the kernels and RCCL
   m.def("range_push", [](const std::string& s) { return roctxRangePushA(s.c_str()); });

@@ -30,21 +30,29 @@ void mv_launch_flat_cast(const void* src, int sd, void* dst, int dd, int64_t n, 
                          int* found_nonfinite, hipStream_t st);
 void mv_launch_sgd(const void* g, int gd, float* w, float* mom, void* model, int md, int64_t n,
                    float lr, float momentum, float dampening, float wd, float gscale, int nesterov,
-                   int first, const float* dyn, hipStream_t st);
+                   int first, const float* dyn, const int* skip, hipStream_t st);
+// skip (nullable): device int32; nonzero => the kernel returns without updating
+// (fp16-wire overflow guard, identical on every rank after the flag allreduce)
 // dyn (nullable): device [lr, first, bc1, bc2] read by the kernel instead of the
 // scalar arguments — HIP-graph replayable hyperparameters (mivod/torch/graphs.py)
 void mv_launch_adam(const void* g, int gd, float* w, float* m, float* v, void* model, int md,
                     int64_t n, float lr, float b1, float b2, float eps, float wd, float gscale,
                     float bc1, float bc2, int adamw, int keras_eps, const float* dyn,
-                    hipStream_t st);
+                    const int* skip, hipStream_t st);
 void mv_launch_adadelta(const void* g, int gd, float* w, float* sq, float* acc, void* model, int md,
                         int64_t n, float lr, float rho, float eps, float wd, float gscale,
-                        const float* dyn, hipStream_t st);
+                        const float* dyn, const int* skip, hipStream_t st);
 void mv_launch_lars(const void* g, int gd, float* w, float* mom, void* model, int md,
                     const ChunkTable& ct, const int32_t* sflag, float* partial, float* norms,
                     float lr, float momentum, float wd, float eta, float gscale, float eps,
-                    int first, const float* dyn, hipStream_t st);
+                    int first, const float* dyn, const int* skip, hipStream_t st);
 void mv_launch_seg_dot3(const void* a, const void* b, int dt, const ChunkTable& ct, float* partial,
                         float* out, hipStream_t st);
 void mv_launch_adasum_combine(void* a, const void* b, int dt, const ChunkTable& ct,
                               const float* dots, hipStream_t st);
+// Adasum (vector halving): per-segment (a.b, |a|^2, |b|^2) with a fp32 and b any dtype
+void mv_launch_seg_dot3_f(const float* a, const void* b, int bdt, const ChunkTable& ct,
+                          float* partial, float* out, hipStream_t st);
+// f <- cf*f + cr*r on the fp32 running merge (swap: f holds b instead of a)
+void mv_launch_adasum_fcombine(float* f, const void* r, int rdt, const ChunkTable& ct,
+                               const float* dots, int swap, hipStream_t st);

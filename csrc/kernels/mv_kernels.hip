@@ -176,7 +176,9 @@ __global__ __launch_bounds__(kBlock) void sgd_flat_kernel(const TG* __restrict__
                                                            float* __restrict__ mom,
                                                            TP* __restrict__ model, int64_t n,
                                                            SgdHp hp,
-                                                           const float* __restrict__ dyn) {
+                                                           const float* __restrict__ dyn,
+                                                           const int* __restrict__ skip) {
+  if (skip && *skip) return;   // overflow guard: every rank skips this step identically
   if (dyn) { hp.lr = dyn[0]; hp.first = dyn[1] != 0.f; }
   const int64_t base = (int64_t)blockIdx.x * kChunk;
   for (int64_t i = base + threadIdx.x * kVec; i < base + kChunk; i += kBlock * kVec) {
@@ -222,7 +224,9 @@ __global__ __launch_bounds__(kBlock) void adam_flat_kernel(const TG* __restrict_
                                                             float* __restrict__ v,
                                                             TP* __restrict__ model, int64_t n,
                                                             AdamHp hp,
-                                                            const float* __restrict__ dyn) {
+                                                            const float* __restrict__ dyn,
+                                                            const int* __restrict__ skip) {
+  if (skip && *skip) return;
   if (dyn) { hp.lr = dyn[0]; hp.bc1 = dyn[2]; hp.bc2 = dyn[3]; }
   const int64_t base = (int64_t)blockIdx.x * kChunk;
   const float step = hp.lr / hp.bc1;
@@ -269,7 +273,9 @@ __global__ __launch_bounds__(kBlock) void adadelta_flat_kernel(const TG* __restr
                                                                 float* __restrict__ acc,
                                                                 TP* __restrict__ model, int64_t n,
                                                                 AdadeltaHp hp,
-                                                                const float* __restrict__ dyn) {
+                                                                const float* __restrict__ dyn,
+                                                                const int* __restrict__ skip) {
+  if (skip && *skip) return;
   if (dyn) hp.lr = dyn[0];
   const int64_t base = (int64_t)blockIdx.x * kChunk;
   for (int64_t i = base + threadIdx.x * kVec; i < base + kChunk; i += kBlock * kVec) {
@@ -388,20 +394,43 @@ __global__ __launch_bounds__(kBlock) void lars_flat_kernel(const TG* __restrict_
                                                             const int32_t* __restrict__ sflag,
                                                             const float* __restrict__ norms,
                                                             LarsHp hp,
-                                                            const float* __restrict__ dyn) {
+                                                            const float* __restrict__ dyn,
+                                                            const int* __restrict__ skip) {
+  if (skip && *skip) return;
   if (dyn) { hp.lr = dyn[0]; hp.first = dyn[1] != 0.f; }
   const int c = blockIdx.x;
   const int64_t beg = cbeg[c];
   const int len = clen[c];
   const int s = cseg[c];
-  const bool skip = sflag[s] & 1;
+  const bool skip_seg = sflag[s] & 1;
   const float wn = sqrtf(norms[2 * s]);
   const float gn = sqrtf(norms[2 * s + 1]);
-  const float wd = skip ? 0.f : hp.wd;
+  const float wd = skip_seg ? 0.f : hp.wd;
   float trust = 1.f;
-  if (!skip && wn > 0.f && gn > 0.f) trust = hp.eta * wn / (gn + wd * wn + hp.eps);
+  if (!skip_seg && wn > 0.f && gn > 0.f) trust = hp.eta * wn / (gn + wd * wn + hp.eps);
   const float slr = hp.lr * trust;
-  for (int i = threadIdx.x; i < len; i += kBlock) {
+  // 8-wide vector body over the 16-byte-aligned prefix (arena segments are
+  // 64-element aligned and chunks start on 4096-element boundaries), scalar tail
+  const int nvec = (aligned16(g + beg) && aligned16(w + beg) && aligned16(mom + beg) &&
+                    (!model || aligned16(model + beg))) ? (len / kVec) * kVec : 0;
+  for (int i = threadIdx.x * kVec; i < nvec; i += kBlock * kVec) {
+    const int64_t k = beg + i;
+    float gv[8], wv[8], mv_[8];
+    load8(g + k, gv);
+    load8(w + k, wv);
+    load8(mom + k, mv_);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float d = gv[j] * hp.gscale + wd * wv[j];
+      float b = hp.first ? slr * d : hp.momentum * mv_[j] + slr * d;
+      mv_[j] = b;
+      wv[j] -= b;
+    }
+    store8(w + k, wv);
+    store8(mom + k, mv_);
+    if (model) store_model(model + k, wv);
+  }
+  for (int i = nvec + threadIdx.x; i < len; i += kBlock) {
     const int64_t k = beg + i;
     float wk = w[k];
     float d = ld1(g + k) * hp.gscale + wd * wk;
@@ -444,6 +473,42 @@ __global__ __launch_bounds__(kBlock) void adasum_combine_kernel(T* __restrict__ 
   }
 }
 
+// Vector-halving Adasum merge on the fp32 running sum f (the wire copy r may be
+// fp16/bf16: only the wire is compressed, the merge stays fp32).
+// swap == 0: f is the lower group's vector a, r is b;  swap == 1: f is b, r is a.
+template <typename TB>
+__global__ __launch_bounds__(kBlock) void adasum_fcombine_kernel(float* __restrict__ f,
+                                                                  const TB* __restrict__ r,
+                                                                  const int64_t* __restrict__ cbeg,
+                                                                  const int32_t* __restrict__ clen,
+                                                                  const int32_t* __restrict__ cseg,
+                                                                  const float* __restrict__ dots,
+                                                                  int swap) {
+  const int c = blockIdx.x;
+  const int64_t beg = cbeg[c];
+  const int len = clen[c];
+  const int s = cseg[c];
+  const float dot = dots[3 * s], na = dots[3 * s + 1], nb = dots[3 * s + 2];
+  const float ca = na >= 1e-8f ? 1.f - dot / (2.f * na) : 1.f;
+  const float cb = nb >= 1e-8f ? 1.f - dot / (2.f * nb) : 1.f;
+  const float cf = swap ? cb : ca;
+  const float cr = swap ? ca : cb;
+  float* fp = f + beg;
+  const TB* rp = r + beg;
+  if (aligned16(fp) && aligned16(rp) && (len % kVec) == 0) {
+    for (int i = threadIdx.x * kVec; i < len; i += kBlock * kVec) {
+      float fv[8], rv[8];
+      load8(fp + i, fv);
+      load8(rp + i, rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fv[j] = cf * fv[j] + cr * rv[j];
+      store8(fp + i, fv);
+    }
+  } else {
+    for (int i = threadIdx.x; i < len; i += kBlock) fp[i] = cf * fp[i] + cr * ld1(rp + i);
+  }
+}
+
 }  // namespace mv
 
 // ---------------- host launchers ----------------
@@ -471,36 +536,37 @@ __global__ __launch_bounds__(kBlock) void adasum_combine_kernel(T* __restrict__ 
 
 void mv_launch_sgd(const void* g, int gd, float* w, float* mom, void* model, int md, int64_t n,
                    float lr, float momentum, float dampening, float wd, float gscale, int nesterov,
-                   int first, const float* dyn, hipStream_t st) {
+                   int first, const float* dyn, const int* skip, hipStream_t st) {
   if (n <= 0) return;
   SgdHp hp{lr, momentum, dampening, wd, gscale, nesterov, first};
   DISPATCH_GP(gd, md, hipLaunchKernelGGL((sgd_flat_kernel<TG, TP>), MV_GRID(n), dim3(kBlock), 0,
-                                         st, (const TG*)g, w, mom, (TP*)model, n, hp, dyn));
+                                         st, (const TG*)g, w, mom, (TP*)model, n, hp, dyn, skip));
 }
 
 void mv_launch_adam(const void* g, int gd, float* w, float* m, float* v, void* model, int md,
                     int64_t n, float lr, float b1, float b2, float eps, float wd, float gscale,
                     float bc1, float bc2, int adamw, int keras_eps, const float* dyn,
-                    hipStream_t st) {
+                    const int* skip, hipStream_t st) {
   if (n <= 0) return;
   AdamHp hp{lr, b1, b2, eps, wd, gscale, bc1, bc2, adamw, keras_eps};
   DISPATCH_GP(gd, md, hipLaunchKernelGGL((adam_flat_kernel<TG, TP>), MV_GRID(n), dim3(kBlock), 0,
-                                         st, (const TG*)g, w, m, v, (TP*)model, n, hp, dyn));
+                                         st, (const TG*)g, w, m, v, (TP*)model, n, hp, dyn, skip));
 }
 
 void mv_launch_adadelta(const void* g, int gd, float* w, float* sq, float* acc, void* model,
                         int md, int64_t n, float lr, float rho, float eps, float wd, float gscale,
-                        const float* dyn, hipStream_t st) {
+                        const float* dyn, const int* skip, hipStream_t st) {
   if (n <= 0) return;
   AdadeltaHp hp{lr, rho, eps, wd, gscale};
   DISPATCH_GP(gd, md, hipLaunchKernelGGL((adadelta_flat_kernel<TG, TP>), MV_GRID(n), dim3(kBlock),
-                                         0, st, (const TG*)g, w, sq, acc, (TP*)model, n, hp, dyn));
+                                         0, st, (const TG*)g, w, sq, acc, (TP*)model, n, hp, dyn,
+                                         skip));
 }
 
 void mv_launch_lars(const void* g, int gd, float* w, float* mom, void* model, int md,
                     const ChunkTable& ct, const int32_t* sflag, float* partial, float* norms,
                     float lr, float momentum, float wd, float eta, float gscale, float eps,
-                    int first, const float* dyn, hipStream_t st) {
+                    int first, const float* dyn, const int* skip, hipStream_t st) {
   if (ct.nchunks <= 0) return;
   // pass 1: per-chunk (|w|^2, |g|^2)
   switch (gd) {
@@ -514,7 +580,7 @@ void mv_launch_lars(const void* g, int gd, float* w, float* mom, void* model, in
   LarsHp hp{lr, momentum, wd, eta, gscale, eps, first};
   DISPATCH_GP(gd, md, hipLaunchKernelGGL((lars_flat_kernel<TG, TP>), dim3(ct.nchunks), dim3(kBlock),
                                          0, st, (const TG*)g, w, mom, (TP*)model, ct.begin, ct.len,
-                                         ct.seg, sflag, norms, hp, dyn));
+                                         ct.seg, sflag, norms, hp, dyn, skip));
 }
 
 void mv_launch_seg_dot3(const void* a, const void* b, int dt, const ChunkTable& ct, float* partial,
@@ -527,6 +593,28 @@ void mv_launch_seg_dot3(const void* a, const void* b, int dt, const ChunkTable& 
   }
   hipLaunchKernelGGL((seg_reduce_kernel<3>), dim3(ct.nseg), dim3(kWave), 0, st, partial, ct.seg_c0,
                      ct.seg_nc, out);
+}
+
+void mv_launch_seg_dot3_f(const float* a, const void* b, int bdt, const ChunkTable& ct,
+                          float* partial, float* out, hipStream_t st) {
+  if (ct.nchunks <= 0) return;
+  switch (bdt) {
+    case F32: hipLaunchKernelGGL((seg_partial_kernel<float, float, 1>), dim3(ct.nchunks), dim3(kBlock), 0, st, a, (const float*)b, ct.begin, ct.len, partial, 1.f); break;
+    case BF16: hipLaunchKernelGGL((seg_partial_kernel<float, __bf16, 1>), dim3(ct.nchunks), dim3(kBlock), 0, st, a, (const __bf16*)b, ct.begin, ct.len, partial, 1.f); break;
+    case F16: hipLaunchKernelGGL((seg_partial_kernel<float, _Float16, 1>), dim3(ct.nchunks), dim3(kBlock), 0, st, a, (const _Float16*)b, ct.begin, ct.len, partial, 1.f); break;
+  }
+  hipLaunchKernelGGL((seg_reduce_kernel<3>), dim3(ct.nseg), dim3(kWave), 0, st, partial, ct.seg_c0,
+                     ct.seg_nc, out);
+}
+
+void mv_launch_adasum_fcombine(float* f, const void* r, int rdt, const ChunkTable& ct,
+                               const float* dots, int swap, hipStream_t st) {
+  if (ct.nchunks <= 0) return;
+  switch (rdt) {
+    case F32: hipLaunchKernelGGL((adasum_fcombine_kernel<float>), dim3(ct.nchunks), dim3(kBlock), 0, st, f, (const float*)r, ct.begin, ct.len, ct.seg, dots, swap); break;
+    case BF16: hipLaunchKernelGGL((adasum_fcombine_kernel<__bf16>), dim3(ct.nchunks), dim3(kBlock), 0, st, f, (const __bf16*)r, ct.begin, ct.len, ct.seg, dots, swap); break;
+    case F16: hipLaunchKernelGGL((adasum_fcombine_kernel<_Float16>), dim3(ct.nchunks), dim3(kBlock), 0, st, f, (const _Float16*)r, ct.begin, ct.len, ct.seg, dots, swap); break;
+  }
 }
 
 void mv_launch_adasum_combine(void* a, const void* b, int dt, const ChunkTable& ct,

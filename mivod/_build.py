@@ -145,6 +145,43 @@ def build_core(verbose: bool = False, force: bool = False) -> str:
     return so
 
 
+def comm_so() -> str:
+    return os.path.join(PKG, "_mvcomm" + EXT_SUFFIX)
+
+
+def _torch_libdir() -> str:
+    import torch
+    return os.path.join(os.path.dirname(torch.__file__), "lib")
+
+
+def build_comm(verbose: bool = False, force: bool = False) -> str:
+    """``mivod/_mvcomm*.so`` — mivod's RCCL data plane (csrc/comm).  Host code
+    only; linked against the librccl / libamdhip64 that PyTorch-ROCm itself
+    loads (same SONAMEs), so one RCCL and one HIP runtime live in the process."""
+    cdir = os.path.join(CSRC, "comm")
+    os.makedirs(BUILD, exist_ok=True)
+    hdrs = _headers(cdir)
+    srcs = sorted(f for f in os.listdir(cdir) if f.endswith(".cc"))
+    objs, jobs = [], []
+    for f in srcs:
+        src = os.path.join(cdir, f)
+        obj = os.path.join(BUILD, "comm_" + f + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src] + hdrs):
+            jobs.append([_hipcc(), "-O2", "-std=c++17", "-fPIC", "-Wall", "-fvisibility=hidden",
+                         "-I", cdir, "-I", os.path.join(ROCM, "include")]
+                        + [x for p in _py_includes() for x in ("-I", p)]
+                        + ["-c", src, "-o", obj])
+    _parallel(jobs, verbose)
+    so = comm_so()
+    tl = _torch_libdir()
+    if force or jobs or _stale(so, objs):
+        _run([_hipcc(), "-shared", "-fPIC", "-o", so] + objs
+             + ["-L", tl, f"-Wl,-rpath,{tl}", "-l:librccl.so", "-l:libamdhip64.so",
+                "-lpthread"], verbose)
+    return so
+
+
 def _parallel(jobs, verbose):
     if not jobs:
         return
@@ -158,6 +195,7 @@ def build_all(verbose: bool = False, force: bool = False) -> list[str]:
     if os.path.isdir(os.path.join(CSRC, "engine")) and any(
             f.endswith(".cc") for f in os.listdir(os.path.join(CSRC, "engine"))):
         out.append(build_core(verbose, force))
+    out.append(build_comm(verbose, force))
     out.append(build_kernels(verbose, force))
     return out
 

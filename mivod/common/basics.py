@@ -6,12 +6,22 @@ by /root/reference/mnist_keras.py:30,35,42,84 and
 
 MI355X design: one process per GPU.  ``init()`` pins the process to GPU
 ``local_rank`` (the reference does this by hand with TF session config,
-mnist_keras.py:32-36), creates the RCCL communicator eagerly through
-``torch.distributed`` (backend "nccl" == RCCL on ROCm, riding xGMI inside a
-node), a gloo group for CPU tensors (metric averaging, tests), and a
-high-priority HIP stream on which every gradient collective and fused optimizer
-step runs, overlapped with backward on the compute stream.  At size 1 no
-network is touched.
+mnist_keras.py:32-36), rendezvouses through torch's TCP store (a gloo world
+that also serves CPU tensors), creates mivod's OWN RCCL communicator eagerly
+(``transport.RcclTransport`` — unique id published by rank 0 in the store,
+``ncclCommInitRank`` in C++, riding xGMI inside a node; horovod's lazy
+NCCL-comm creation), intra-/cross-node child comms by
+``ncclCommSplit`` for hierarchical allreduce, the native TCP rings for CPU
+tensors, and a high-priority HIP stream on which every GPU collective — the
+gradient buckets and the engine's named ops alike, in one cross-rank-agreed
+order (``parallel.order``) — and every fused optimizer step runs, overlapped
+with backward on the compute stream.  At size 1 no network is touched
+(``MIVOD_FORCE_COLLECTIVES=1`` still builds a 1-rank RCCL comm so the GPU
+collective path can be exercised on one GPU).
+
+``MIVOD_TRANSPORT``: ``rccl`` (default with a GPU) | ``torch`` (torch's
+ProcessGroupNCCL, A/B only) | ``gloo-gpu`` (GPU compute, gloo wire — several
+ranks on ONE GPU, the multi-rank GPU test mode) | ``gloo`` / ``cpu`` (no GPU).
 """
 from __future__ import annotations
 
@@ -43,12 +53,14 @@ class _State:
         self.config: Config | None = None
         self.device = torch.device("cpu")
         self.backend = "none"
-        self.pg = None           # main (GPU / default) group
+        self.pg = None           # torch.distributed world (rendezvous, CPU fallback)
         self.cpu_pg = None       # gloo group for CPU tensors
-        self.engine_pg = None    # group used by the negotiated named-op engine
-        self.engine_cpu_pg = None
-        self.local_pg = None     # intra-node group (hierarchical ops)
+        self.engine_cpu_pg = None  # gloo group for the named-op engine's CPU tensors
+        self.local_pg = None     # intra-node gloo group (hierarchical CPU ops)
         self.cross_pg = None     # one rank per node with equal local_rank
+        self.gpu = None          # GPU transport (RcclTransport / PgTransport)
+        self.gpu_local = None    # ncclCommSplit intra-node child
+        self.gpu_cross = None    # ncclCommSplit cross-node child
         self.comm_stream = None
         self.rings = None        # native CPU data plane: [main ring, engine ring] (tcp_ring.py)
         self.init_count = 0
@@ -103,7 +115,7 @@ def resolve_topology(env=None) -> dict:
 
 
 def _gpu_available() -> bool:
-    if os.environ.get("MIVOD_TRANSPORT", "").lower() in ("gloo", "tcp", "cpu"):
+    if os.environ.get("MIVOD_TRANSPORT", "").lower() in ("gloo", "tcp", "cpu", "local"):
         return False
     try:
         return torch.cuda.is_available() and torch.cuda.device_count() > 0
@@ -153,35 +165,42 @@ def init(comm=None, process_sets=None):
             _state.device = torch.device("cpu")
 
         transport = cfg.transport or ("rccl" if use_gpu else "gloo")
+        if transport == "nccl":
+            transport = "rccl"
+        from ..parallel.order import ORDER
+        _state.gpu = _state.gpu_local = _state.gpu_cross = None
+        _state.init_count += 1
         if _state.size > 1:
             if not dist.is_initialized():
-                backend = "nccl" if (use_gpu and transport in ("rccl", "nccl")) else "gloo"
+                backend = "nccl" if (use_gpu and transport == "torch") else "gloo"
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29500")
                 kwargs = dict(backend=backend, rank=_state.rank, world_size=_state.size,
                               timeout=datetime.timedelta(
                                   seconds=float(os.environ.get("MIVOD_INIT_TIMEOUT_S", "600"))))
                 if backend == "nccl":
-                    kwargs["device_id"] = _state.device   # eager RCCL communicator init (C5/C6)
+                    kwargs["device_id"] = _state.device
                 dist.init_process_group(**kwargs)
-            _state.backend = dist.get_backend()
+            world_backend = dist.get_backend()
             _state.pg = dist.group.WORLD
-            if _state.backend == "gloo":
-                _state.cpu_pg = _state.pg
-            else:
-                _state.cpu_pg = dist.new_group(backend="gloo")
-            # Separate communicators for the negotiated engine so that its
-            # background-thread collectives never interleave with the static
-            # gradient schedule issued from backward hooks.
-            _state.engine_pg = dist.new_group(backend=_state.backend) if _state.backend != "gloo" \
-                else dist.new_group(backend="gloo")
+            _state.cpu_pg = _state.pg if world_backend == "gloo" else dist.new_group(backend="gloo")
+            # the engine's CPU named ops get their own gloo group / TCP ring so they
+            # never interleave on a socket with the caller thread's CPU collectives
             _state.engine_cpu_pg = dist.new_group(backend="gloo")
             _make_hierarchy_groups()
             from ..parallel.tcp_ring import make_rings
-            _state.init_count += 1
             _state.rings = make_rings(_state, generation=_state.init_count)
+            if use_gpu:
+                _make_gpu_plane(transport, world_backend, cfg)
+            else:
+                _state.backend = "gloo"
         else:
             _state.backend = "local"
+            if use_gpu and os.environ.get("MIVOD_FORCE_COLLECTIVES", "0") == "1":
+                from ..parallel.transport import RcclTransport
+                _state.gpu = RcclTransport.create(0, 1, _state.device)
+                _state.backend = "rccl"
+        ORDER.reset(enabled=_state.gpu is not None and _state.size > 1)
         _state.initialized = True
 
         from ..parallel.engine import Engine
@@ -190,13 +209,59 @@ def init(comm=None, process_sets=None):
         atexit.register(shutdown)
 
 
+def _hierarchical_topology() -> bool:
+    ls, cs = _state.local_size, _state.cross_size
+    return ls * cs == _state.size and ls != _state.size and ls != 1
+
+
+def _make_gpu_plane(transport: str, world_backend: str, cfg) -> None:
+    """The GPU transport of a multi-rank world (+ hierarchical children)."""
+    from ..parallel.transport import PgTransport, RcclTransport
+    if transport == "rccl":
+        store = dist.distributed_c10d._get_default_store()
+        timeout = float(os.environ.get("MIVOD_RCCL_TIMEOUT_S", cfg.stall_shutdown_time_s or 0.0))
+        _state.gpu = RcclTransport.create(
+            _state.rank, _state.size, _state.device, store,
+            key=f"mivod/rccl/{_state.init_count}", timeout_s=timeout,
+            exit_on_abort=cfg.stall_shutdown_time_s > 0)
+        _state.backend = "rccl"
+        if _hierarchical_topology():
+            _state.gpu_local = _state.gpu.split(_state.cross_rank, _state.local_rank)
+            _state.gpu_cross = _state.gpu.split(_state.local_rank, _state.cross_rank)
+        return
+    if transport == "torch":
+        pg = _state.pg if world_backend == "nccl" else dist.new_group(backend="nccl")
+        _state.gpu = PgTransport(pg, staged=False, name="torch-nccl")
+        _state.backend = "torch-nccl"
+        sub_backend, staged = "nccl", False
+    elif transport in ("gloo-gpu", "gloo_gpu"):
+        _state.gpu = PgTransport(dist.new_group(backend="gloo"), staged=True, name="gloo-gpu")
+        _state.backend = "gloo-gpu"
+        sub_backend, staged = "gloo", True
+    else:
+        raise ValueError(f"unknown MIVOD_TRANSPORT={transport!r} "
+                         "(rccl | torch | gloo-gpu | gloo)")
+    if _hierarchical_topology():
+        ls, cs = _state.local_size, _state.cross_size
+        for node in range(cs):
+            ranks = list(range(node * ls, (node + 1) * ls))
+            g = dist.new_group(ranks=ranks, backend=sub_backend)
+            if _state.rank in ranks:
+                _state.gpu_local = PgTransport(g, staged=staged, name=_state.gpu.name)
+        for lr in range(ls):
+            ranks = [node * ls + lr for node in range(cs)]
+            g = dist.new_group(ranks=ranks, backend=sub_backend)
+            if _state.rank in ranks:
+                _state.gpu_cross = PgTransport(g, staged=staged, name=_state.gpu.name)
+
+
 def _make_hierarchy_groups():
-    """Intra-node and cross-node groups (for hierarchical allreduce / Adasum).
+    """Intra-node and cross-node gloo groups (hierarchical CPU allreduce).
     Every rank must create every group, in the same order."""
     ls, cs = _state.local_size, _state.cross_size
-    if ls * cs != _state.size or ls == _state.size or ls == 1:
+    if not _hierarchical_topology():
         return
-    backend = _state.backend
+    backend = "gloo"
     for node in range(cs):
         ranks = list(range(node * ls, (node + 1) * ls))
         g = dist.new_group(ranks=ranks, backend=backend)
@@ -229,13 +294,20 @@ def shutdown():
             for r in _state.rings:
                 r.close()
             _state.rings = None
+        for tr in (_state.gpu_local, _state.gpu_cross, _state.gpu):
+            if tr is not None:
+                try:
+                    tr.close()
+                except Exception as e:  # pragma: no cover
+                    log.warning("mivod GPU transport shutdown error: %s", e)
+        _state.gpu = _state.gpu_local = _state.gpu_cross = None
         if _state.owns_pg and dist.is_initialized():
             try:
                 dist.destroy_process_group()
             except Exception:  # pragma: no cover
                 pass
         _state.initialized = False
-        _state.pg = _state.cpu_pg = _state.engine_pg = _state.engine_cpu_pg = None
+        _state.pg = _state.cpu_pg = _state.engine_cpu_pg = None
         _state.local_pg = _state.cross_pg = None
 
 
@@ -293,8 +365,12 @@ def gloo_enabled() -> bool:
 
 
 def nccl_built() -> bool:
-    """True when the RCCL (torch 'nccl') backend is available."""
-    return dist.is_available() and dist.is_nccl_available()
+    """True when mivod's RCCL data plane (mivod._mvcomm) is importable."""
+    try:
+        from .. import _mvcomm  # noqa: F401
+        return True
+    except ImportError:
+        return False
 
 
 def rocm_built() -> bool:

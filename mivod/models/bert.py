@@ -119,8 +119,10 @@ class BertModel(nn.Module):
 
     def forward(self, input_ids, token_type_ids, attention_mask=None):
         x = self.embeddings(input_ids, token_type_ids)
+        # built whenever a mask is given — no data-dependent host sync per forward
+        # (packed pre-training batches pass attention_mask=None: every token valid)
         mask_bias = None
-        if attention_mask is not None and not bool(attention_mask.all()):
+        if attention_mask is not None:
             mask_bias = (1.0 - attention_mask[:, None, None, :].to(x.dtype)) * -10000.0
         for lyr in self.layers:
             x = lyr(x, mask_bias)
@@ -170,12 +172,14 @@ class BertForPreTraining(nn.Module):
 
 
 def synthetic_batch(c: BertConfig, batch: int, seq: int, device, mask_frac=0.15,
-                    generator=None):
+                    generator=None, with_mask: bool = False):
+    """Synthetic pre-training batch of full-length (packed) sequences: the
+    attention mask is None (every position valid) unless ``with_mask``."""
     g = generator
     ids = torch.randint(0, c.vocab_size, (batch, seq), device=device, generator=g)
     tt = torch.zeros(batch, seq, dtype=torch.long, device=device)
     tt[:, seq // 2:] = 1
-    am = torch.ones(batch, seq, dtype=torch.long, device=device)
+    am = torch.ones(batch, seq, dtype=torch.long, device=device) if with_mask else None
     m = max(1, int(round(seq * mask_frac)))
     pos = torch.stack([torch.randperm(seq, device=device, generator=g)[:m]
                        for _ in range(batch)]).sort(dim=1).values

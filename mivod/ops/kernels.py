@@ -116,13 +116,21 @@ def flat_cast(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0,
 # ---------------------------------------------------------------------------
 # K6 fused optimizers (flat)
 # ---------------------------------------------------------------------------
+def _skipped(skip) -> bool:
+    return skip is not None and int(skip.reshape(-1)[0]) != 0
+
+
 def sgd_step(g, w, mom, model, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0,
-             gscale=1.0, nesterov=False, first=False, dyn=None):
+             gscale=1.0, nesterov=False, first=False, dyn=None, skip=None):
     """``dyn`` (GPU only): device fp32 [lr, first, bc1, bc2] read by the kernel in
-    place of ``lr`` / ``first`` — the HIP-graph replay path (mivod.torch.graphs)."""
+    place of ``lr`` / ``first`` — the HIP-graph replay path (mivod.torch.graphs).
+    ``skip``: device int32 flag; nonzero => no update (fp16-wire overflow guard)."""
     if _on_gpu(g):
         native().sgd_step(g, w, mom, model, float(lr), float(momentum), float(dampening),
-                          float(weight_decay), float(gscale), bool(nesterov), bool(first), dyn)
+                          float(weight_decay), float(gscale), bool(nesterov), bool(first), dyn,
+                          skip)
+        return
+    if _skipped(skip):
         return
     d = g.float() * gscale + weight_decay * w
     if mom is not None:
@@ -137,11 +145,13 @@ def sgd_step(g, w, mom, model, *, lr, momentum=0.0, dampening=0.0, weight_decay=
 
 
 def adam_step(g, w, m, v, model, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
-              gscale=1.0, step=1, adamw=False, keras_eps=False, dyn=None):
+              gscale=1.0, step=1, adamw=False, keras_eps=False, dyn=None, skip=None):
     if _on_gpu(g):
         native().adam_step(g, w, m, v, model, float(lr), float(beta1), float(beta2), float(eps),
                            float(weight_decay), float(gscale), int(step), bool(adamw),
-                           bool(keras_eps), dyn)
+                           bool(keras_eps), dyn, skip)
+        return
+    if _skipped(skip):
         return
     gr = g.float() * gscale
     if not adamw and weight_decay:
@@ -162,10 +172,12 @@ def adam_step(g, w, m, v, model, *, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight
 
 
 def adadelta_step(g, w, sq, acc, model, *, lr=1.0, rho=0.9, eps=1e-6, weight_decay=0.0,
-                  gscale=1.0, dyn=None):
+                  gscale=1.0, dyn=None, skip=None):
     if _on_gpu(g):
         native().adadelta_step(g, w, sq, acc, model, float(lr), float(rho), float(eps),
-                               float(weight_decay), float(gscale), dyn)
+                               float(weight_decay), float(gscale), dyn, skip)
+        return
+    if _skipped(skip):
         return
     gr = g.float() * gscale + weight_decay * w
     sq.mul_(rho).addcmul_(gr, gr, value=1 - rho)
@@ -229,11 +241,20 @@ def make_chunk_table(seg_sizes: Sequence[int], device, seg_offsets: Optional[Seq
                       list(map(int, seg_offsets)), int(total))
 
 
+def _check_table(table: ChunkTable, numel: int) -> None:
+    """Host-side bound check before a segmented launch: every chunk of the
+    table must lie inside the buffers the kernel will index."""
+    if table.total > numel:
+        raise ValueError(f"mivod: chunk table covers {table.total} elements but the buffer "
+                         f"has {numel}")
+
+
 def lars_step(g, w, mom, model, table: ChunkTable, seg_flags: torch.Tensor, *, lr, momentum=0.9,
               weight_decay=0.0, eta=0.001, gscale=1.0, eps=0.0, first=False,
-              workspace: Optional[dict] = None, dyn=None):
+              workspace: Optional[dict] = None, dyn=None, skip=None):
     """Segmented LARS (You et al. 2017): per segment trust = eta*|w|/(|g|+wd*|w|);
     flagged segments (bit0) get trust 1 and no weight decay."""
+    _check_table(table, g.numel())
     if _on_gpu(g):
         ws = workspace if workspace is not None else {}
         partial = ws.get("partial")
@@ -246,7 +267,9 @@ def lars_step(g, w, mom, model, table: ChunkTable, seg_flags: torch.Tensor, *, l
         native().lars_step(g, w, mom, model, table.begin, table.len, table.seg, table.seg_c0,
                            table.seg_nc, seg_flags, partial, norms, float(lr), float(momentum),
                            float(weight_decay), float(eta), float(gscale), float(eps), bool(first),
-                           dyn)
+                           dyn, skip)
+        return
+    if _skipped(skip):
         return
     flags = seg_flags.tolist()
     for i, (off, n) in enumerate(zip(table.seg_offsets, table.seg_sizes)):
@@ -270,7 +293,9 @@ def lars_step(g, w, mom, model, table: ChunkTable, seg_flags: torch.Tensor, *, l
 
 def seg_dot3(a: torch.Tensor, b: torch.Tensor, table: ChunkTable,
              workspace: Optional[dict] = None) -> torch.Tensor:
-    """Per segment (a.b, |a|^2, |b|^2) as a [nseg, 3] fp32 tensor (deterministic)."""
+    """Per segment (a.b, |a|^2, |b|^2) as a [nseg, 3] fp32 tensor (deterministic).
+    ``a`` may be fp32 while ``b`` is the (fp16/bf16) wire copy."""
+    _check_table(table, min(a.numel(), b.numel()))
     if _on_gpu(a):
         ws = workspace if workspace is not None else {}
         partial = ws.get("partial3")
@@ -290,6 +315,7 @@ def seg_dot3(a: torch.Tensor, b: torch.Tensor, table: ChunkTable,
 
 def adasum_combine(a: torch.Tensor, b: torch.Tensor, table: ChunkTable, dots: torch.Tensor) -> None:
     """a <- (1 - d/(2|a|^2)) a + (1 - d/(2|b|^2)) b per segment."""
+    _check_table(table, min(a.numel(), b.numel()))
     if _on_gpu(a):
         native().adasum_combine(a, b, table.begin, table.len, table.seg, table.seg_c0,
                                 table.seg_nc, dots.reshape(-1).contiguous())
@@ -301,3 +327,25 @@ def adasum_combine(a: torch.Tensor, b: torch.Tensor, table: ChunkTable, dots: to
         cb = 1.0 - dot / (2 * nb) if nb >= 1e-8 else 1.0
         x = a[off:off + n]
         x.copy_(ca * x.float() + cb * b[off:off + n].float())
+
+
+def adasum_fcombine(f: torch.Tensor, r: torch.Tensor, table: ChunkTable, dots: torch.Tensor,
+                    swap: bool) -> None:
+    """Vector-halving Adasum merge on the fp32 running sum ``f`` with the received
+    (wire-dtype) copy ``r``: ``dots`` rows are (a.b, |a|^2, |b|^2) with a = the
+    lower rank group's vector; ``swap`` means ``f`` holds b.  f <- ca*a + cb*b."""
+    _check_table(table, min(f.numel(), r.numel()))
+    if _on_gpu(f):
+        native().adasum_fcombine(f, r, table.begin, table.len, table.seg, table.seg_c0,
+                                 table.seg_nc, dots.reshape(-1).contiguous(), bool(swap))
+        return
+    d = dots.reshape(-1, 3).tolist()
+    for i, (off, n) in enumerate(zip(table.seg_offsets, table.seg_sizes)):
+        if n <= 0:
+            continue
+        dot, na, nb = d[i]
+        ca = 1.0 - dot / (2 * na) if na >= 1e-8 else 1.0
+        cb = 1.0 - dot / (2 * nb) if nb >= 1e-8 else 1.0
+        cf, cr = (cb, ca) if swap else (ca, cb)
+        x = f[off:off + n]
+        x.copy_(cf * x + cr * r[off:off + n].float())

@@ -118,6 +118,7 @@ class FusedOptimizer(torch.optim.Optimizer):
         self._mv_grad_dtype = grad_dtype
         self._mv_external_grads = False   # True when DistributedOptimizer packs grads
         self._mv_graph = False            # True while a HIP graph captures the step
+        self._mv_skip = None              # device int32 skip flag (overflow guard)
 
     # ---- layout ----------------------------------------------------------
     def _mv_build(self, grad_dtype_for=None) -> List[Arena]:
@@ -218,13 +219,21 @@ class FusedOptimizer(torch.optim.Optimizer):
 
     def load_state_dict(self, state_dict):
         arenas = self._mv_build()
+        # torch's loader casts every floating state tensor to its parameter's dtype
+        # (bf16 for a bf16 model): take the exact fp32 values (master weights, Adam
+        # moments) from the incoming dict instead of from the cast copies
+        raw = {}
+        for g_saved, g_live in zip(state_dict.get("param_groups", []), self.param_groups):
+            for k, p in zip(g_saved["params"], g_live["params"]):
+                if k in state_dict.get("state", {}):
+                    raw[p] = state_dict["state"][k]
         super().load_state_dict(state_dict)
         # torch replaced our views with fresh tensors: copy them back into the arenas
         with torch.no_grad():
             for a in arenas:
                 steps = []
                 for i, p in enumerate(a.params):
-                    st = self.state.get(p, {})
+                    st = raw.get(p) or self.state.get(p, {})
                     for n, flat in a.state.items():
                         if n in st and torch.is_tensor(st[n]):
                             a.slot(flat, i).copy_(st[n])
@@ -261,7 +270,8 @@ class FusedSGD(FusedOptimizer):
         hp = a.group
         K.sgd_step(g, w, st.get("momentum_buffer"), model, lr=hp["lr"], momentum=hp["momentum"],
                    dampening=hp["dampening"], weight_decay=hp["weight_decay"], gscale=gscale,
-                   nesterov=hp["nesterov"], first=(a.step == 1), dyn=self._mv_dyn(a))
+                   nesterov=hp["nesterov"], first=(a.step == 1), dyn=self._mv_dyn(a),
+                   skip=self._mv_skip)
 
 
 class FusedAdam(FusedOptimizer):
@@ -281,7 +291,8 @@ class FusedAdam(FusedOptimizer):
         b1, b2 = hp["betas"]
         K.adam_step(g, w, st["exp_avg"], st["exp_avg_sq"], model, lr=hp["lr"], beta1=b1, beta2=b2,
                     eps=hp["eps"], weight_decay=hp["weight_decay"], gscale=gscale, step=a.step,
-                    adamw=hp["adamw"], keras_eps=hp["keras_eps"], dyn=self._mv_dyn(a))
+                    adamw=hp["adamw"], keras_eps=hp["keras_eps"], dyn=self._mv_dyn(a),
+                    skip=self._mv_skip)
 
 
 class FusedAdamW(FusedAdam):
@@ -304,7 +315,7 @@ class FusedAdadelta(FusedOptimizer):
         hp = a.group
         K.adadelta_step(g, w, st["square_avg"], st["acc_delta"], model, lr=hp["lr"], rho=hp["rho"],
                         eps=hp["eps"], weight_decay=hp["weight_decay"], gscale=gscale,
-                        dyn=self._mv_dyn(a))
+                        dyn=self._mv_dyn(a), skip=self._mv_skip)
 
 
 class FusedLARS(FusedOptimizer):
@@ -331,4 +342,4 @@ class FusedLARS(FusedOptimizer):
         K.lars_step(g, w, st["momentum_buffer"], model, a.table(i0, i1), flags, lr=hp["lr"],
                     momentum=hp["momentum"], weight_decay=hp["weight_decay"], eta=hp["eta"],
                     gscale=gscale, eps=hp["eps"], first=(a.step == 1), workspace=a.workspace,
-                    dyn=self._mv_dyn(a))
+                    dyn=self._mv_dyn(a), skip=self._mv_skip)

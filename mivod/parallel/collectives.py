@@ -1,13 +1,18 @@
-"""Flat-buffer collectives on the mivod process groups.
+"""Flat-buffer collectives — the data plane under both the static gradient
+schedule (``mivod.torch.DistributedOptimizer``) and the negotiated named-op
+engine.
 
-This is the data plane under both the static gradient schedule
-(``mivod.torch.DistributedOptimizer``) and the negotiated named-op engine.
-GPU tensors ride RCCL (torch.distributed backend "nccl" == RCCL on ROCm) over
-xGMI; CPU tensors ride gloo.  Callers choose the HIP stream (the comm stream);
-a collective here never blocks the host for GPU tensors.
+GPU tensors ride mivod's own RCCL communicator (``transport.RcclTransport``,
+csrc/comm) over xGMI on the caller's HIP stream (the comm stream); every GPU
+collective is one entry of the cross-rank issue order (``order.ORDER``), so the
+hook-driven bucket schedule and the engine's named ops can share ONE
+communicator without deadlocking.  CPU tensors ride the native TCP ring
+(csrc/engine/ring.cc) or gloo.  A collective never blocks the host for GPU
+tensors (RCCL transport).
 
-Horovod parity: allreduce (Sum / Average / Adasum),
-allgather (first-dim concat, ragged allowed), broadcast.
+Horovod parity: allreduce (Sum / Average / Adasum, plus
+pre-scale), hierarchical allreduce, allgather (first-dim concat, ragged
+allowed), broadcast, alltoall, barrier.
 """
 from __future__ import annotations
 
@@ -17,13 +22,18 @@ import torch
 import torch.distributed as dist
 
 from ..common import basics
+from . import transport as T
+from .order import ORDER
 
-# horovod reduce ops (horovod/common/basics.py: Average / Sum / Adasum)
+# horovod reduce ops (horovod/common/basics.py: Average / Sum / Adasum) + internal Max/Min
 Average = 0
 Sum = 1
 Adasum = 2
+Max = 3
+Min = 4
 
-_OP_NAMES = {Average: "Average", Sum: "Sum", Adasum: "Adasum"}
+_OP_NAMES = {Average: "Average", Sum: "Sum", Adasum: "Adasum", Max: "Max", Min: "Min"}
+_TOP = {Average: T.AVG, Sum: T.SUM, Max: T.MAX, Min: T.MIN}
 
 
 def op_name(op: int) -> str:
@@ -34,10 +44,13 @@ def _gloo_ok(dtype: torch.dtype) -> bool:
     return dtype not in (torch.bfloat16,)
 
 
-def _native_gpu(t: torch.Tensor) -> bool:
-    """GPU tensor on an RCCL world (False for MIVOD_TRANSPORT=gloo-gpu: GPU compute,
-    gloo wire — the multi-rank-on-one-GPU test mode, which lacks AVG and bf16)."""
-    return t.is_cuda and basics.state().backend != "gloo"
+def _gpu_transport(t: torch.Tensor, group=None):
+    """The GPU transport serving ``t`` (None for CPU tensors / no GPU plane)."""
+    if not t.is_cuda:
+        return None
+    if group is not None and hasattr(group, "allreduce_"):
+        return group
+    return basics.state().gpu
 
 
 def _ring(t: torch.Tensor, group, engine: bool):
@@ -52,36 +65,54 @@ def _ring(t: torch.Tensor, group, engine: bool):
 
 def group_for(t: torch.Tensor, engine: bool = False):
     st = basics.state()
-    if t.is_cuda:
-        return st.engine_pg if engine else st.pg
     return st.engine_cpu_pg if engine else st.cpu_pg
 
 
+def _flat(t: torch.Tensor) -> torch.Tensor:
+    return t.view(-1) if t.is_contiguous() else t.contiguous().view(-1)
+
+
 def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
-               adasum_table=None) -> torch.Tensor:
+               adasum_table=None, prescale: float = 1.0) -> torch.Tensor:
     """In-place allreduce of a dense tensor.  ``Average`` divides by size
-    (RCCL ncclAvg on GPU).  Adasum needs a chunk table of the per-tensor
+    (ncclAvg on GPU), ``prescale`` multiplies every rank's contribution first
+    (ncclRedOpCreatePreMulSum).  Adasum needs a chunk table of the per-tensor
     segments (``ops.kernels.make_chunk_table``)."""
     st = basics.state()
+    tr = _gpu_transport(t, group)
+    if tr is not None:
+        with ORDER.issue(negotiated=engine):
+            flat = _flat(t)
+            if op == Adasum:
+                from .adasum import adasum_allreduce_
+                if prescale != 1.0:
+                    flat.mul_(prescale)
+                adasum_allreduce_(flat, adasum_table, tr)
+            elif (st.config is not None and st.config.hierarchical_allreduce and group is None
+                  and st.gpu_local is not None and st.gpu_cross is not None):
+                _hierarchical_gpu_(flat, op, prescale)
+            else:
+                tr.allreduce_(flat, _TOP[op], prescale)
+            if flat.data_ptr() != t.data_ptr():
+                t.copy_(flat.view_as(t))
+        return t
+    if prescale != 1.0:
+        t.mul_(prescale)
     if st.size == 1:
         return t
     pg = group or group_for(t, engine)
     if op == Adasum:
         from .adasum import adasum_allreduce_
-        return adasum_allreduce_(t, adasum_table, pg)
+        return adasum_allreduce_(t, adasum_table)
     if (st.config is not None and st.config.hierarchical_allreduce and st.local_pg is not None
-            and st.cross_pg is not None and group is None and not engine
-            and t.is_cuda == (st.backend == "nccl")):
-        return hierarchical_allreduce_(t, op)
-    if t.is_cuda and st.backend != "gloo":
-        rop = dist.ReduceOp.AVG if op == Average else dist.ReduceOp.SUM
-        dist.all_reduce(t, op=rop, group=pg)
-        return t
+            and st.cross_pg is not None and group is None and not engine):
+        return _hierarchical_cpu_(t, op)
     ring = _ring(t, group, engine)
-    if ring is not None:
+    if ring is not None and op in (Average, Sum):
         return ring.allreduce_(t, average=(op == Average))
+    rop = {Max: dist.ReduceOp.MAX, Min: dist.ReduceOp.MIN}.get(op, dist.ReduceOp.SUM)
     if _gloo_ok(t.dtype):
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg)
+        dist.all_reduce(t, op=rop, group=pg)
         if op == Average:
             if t.dtype.is_floating_point:
                 t.div_(st.size)
@@ -89,37 +120,43 @@ def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
                 t.floor_divide_(st.size)
         return t
     w = t.float()
-    dist.all_reduce(w, op=dist.ReduceOp.SUM, group=pg)
+    dist.all_reduce(w, op=rop, group=pg)
     if op == Average:
         w.div_(st.size)
     t.copy_(w)
     return t
 
 
-def hierarchical_allreduce_(t: torch.Tensor, op: int = Sum) -> torch.Tensor:
-    """HOROVOD_HIERARCHICAL_ALLREDUCE: intra-node reduce-scatter (xGMI), cross-node
-    allreduce of each 1/local_size shard (the network carries 1/L of the bytes),
-    intra-node allgather.  On CPU/gloo (no reduce-scatter) the same two-level
-    structure runs as local allreduce + cross allreduce."""
+def _hierarchical_gpu_(flat: torch.Tensor, op: int, prescale: float) -> None:
+    """HOROVOD_HIERARCHICAL_ALLREDUCE on GPU: intra-node reduce-scatter (xGMI),
+    cross-node allreduce of each 1/local_size shard (the network carries 1/L of
+    the bytes), intra-node allgather — three RCCL calls on ncclCommSplit comms."""
     st = basics.state()
-    L = st.local_size
-    flat = t.view(-1) if t.is_contiguous() else t.contiguous().view(-1)
-    if t.is_cuda:
-        n = flat.numel()
-        pad = (-n) % L
-        work = flat if pad == 0 else torch.cat([flat, flat.new_zeros(pad)])
-        shard = torch.empty(work.numel() // L, dtype=t.dtype, device=t.device)
-        dist.reduce_scatter_tensor(shard, work, op=dist.ReduceOp.SUM, group=st.local_pg)
-        dist.all_reduce(shard, op=dist.ReduceOp.SUM, group=st.cross_pg)
-        dist.all_gather_into_tensor(work, shard, group=st.local_pg)
-        if pad:
-            flat.copy_(work[:n])
-    else:
-        work = flat if _gloo_ok(flat.dtype) else flat.float()
-        dist.all_reduce(work, op=dist.ReduceOp.SUM, group=st.local_pg)
-        dist.all_reduce(work, op=dist.ReduceOp.SUM, group=st.cross_pg)
-        if work is not flat:
-            flat.copy_(work)
+    L = st.gpu_local.size
+    if prescale != 1.0:
+        flat.mul_(prescale)
+    n = flat.numel()
+    pad = (-n) % L
+    work = flat if pad == 0 else torch.cat([flat, flat.new_zeros(pad)])
+    shard = torch.empty(work.numel() // L, dtype=flat.dtype, device=flat.device)
+    st.gpu_local.reduce_scatter(shard, work, T.SUM)
+    st.gpu_cross.allreduce_(shard, T.SUM)
+    st.gpu_local.allgather_into(work, shard)
+    if pad:
+        flat.copy_(work[:n])
+    if op == Average:
+        flat.div_(st.size)
+
+
+def _hierarchical_cpu_(t: torch.Tensor, op: int = Sum) -> torch.Tensor:
+    """The same two-level structure on CPU/gloo (local allreduce + cross allreduce)."""
+    st = basics.state()
+    flat = _flat(t)
+    work = flat if _gloo_ok(flat.dtype) else flat.float()
+    dist.all_reduce(work, op=dist.ReduceOp.SUM, group=st.local_pg)
+    dist.all_reduce(work, op=dist.ReduceOp.SUM, group=st.cross_pg)
+    if work is not flat:
+        flat.copy_(work)
     if op == Average:
         flat.div_(st.size)
     if flat.data_ptr() != t.data_ptr():
@@ -127,25 +164,56 @@ def hierarchical_allreduce_(t: torch.Tensor, op: int = Sum) -> torch.Tensor:
     return t
 
 
+def hierarchical_allreduce_(t: torch.Tensor, op: int = Sum) -> torch.Tensor:
+    st = basics.state()
+    if t.is_cuda and st.gpu_local is not None and st.gpu_cross is not None:
+        with ORDER.issue():
+            flat = _flat(t)
+            _hierarchical_gpu_(flat, op, 1.0)
+            if flat.data_ptr() != t.data_ptr():
+                t.copy_(flat.view_as(t))
+        return t
+    return _hierarchical_cpu_(t, op)
+
+
 def allgather(t: torch.Tensor, group=None, engine: bool = False) -> torch.Tensor:
     """Concatenate ``t`` from every rank along dim 0 (first dims may differ)."""
     st = basics.state()
-    if st.size == 1:
+    tr = _gpu_transport(t, group)
+    if tr is not None and tr.size > 1:
+        with ORDER.issue(negotiated=engine):
+            src = (t if t.dim() > 0 else t.reshape(1)).contiguous()
+            n = torch.tensor([src.shape[0]], dtype=torch.int64, device=t.device)
+            sizes_t = torch.empty(tr.size, dtype=torch.int64, device=t.device)
+            tr.allgather_into(sizes_t, n)
+            sizes = sizes_t.tolist()
+            rest = tuple(src.shape[1:])
+            mx = max(sizes)
+            if all(s == mx for s in sizes):
+                out = torch.empty((mx * tr.size,) + rest, dtype=src.dtype, device=src.device)
+                tr.allgather_into(out, src)
+                return out
+            pad = torch.zeros((mx,) + rest, dtype=src.dtype, device=src.device)
+            pad[:src.shape[0]].copy_(src)
+            outs = torch.empty((mx * tr.size,) + rest, dtype=src.dtype, device=src.device)
+            tr.allgather_into(outs, pad)
+            parts = outs.view((tr.size, mx) + rest)
+            return torch.cat([parts[i, :s] for i, s in enumerate(sizes)], dim=0)
+    if st.size == 1 or tr is not None:
         return t.clone()
     ring = _ring(t, group, engine)
     if ring is not None:
         return ring.allgather(t)
     pg = group or group_for(t, engine)
-    n = torch.tensor([t.shape[0] if t.dim() > 0 else 1], dtype=torch.int64,
-                     device=t.device if t.is_cuda else "cpu")
+    n = torch.tensor([t.shape[0] if t.dim() > 0 else 1], dtype=torch.int64)
     sizes = [torch.zeros_like(n) for _ in range(st.size)]
     dist.all_gather(sizes, n, group=pg)
     sizes = [int(s.item()) for s in sizes]
     src = t if t.dim() > 0 else t.reshape(1)
     rest = tuple(src.shape[1:])
     mx = max(sizes)
-    work_dtype = src.dtype if (_native_gpu(t) or _gloo_ok(src.dtype)) else torch.float32
-    pad = torch.zeros((mx,) + rest, dtype=work_dtype, device=src.device)
+    work_dtype = src.dtype if _gloo_ok(src.dtype) else torch.float32
+    pad = torch.zeros((mx,) + rest, dtype=work_dtype)
     pad[:src.shape[0]].copy_(src)
     outs = [torch.empty_like(pad) for _ in range(st.size)]
     dist.all_gather(outs, pad, group=pg)
@@ -155,13 +223,23 @@ def allgather(t: torch.Tensor, group=None, engine: bool = False) -> torch.Tensor
 
 def broadcast_(t: torch.Tensor, root_rank: int, group=None, engine: bool = False) -> torch.Tensor:
     st = basics.state()
+    tr = _gpu_transport(t, group)
+    if tr is not None:
+        if tr.size == 1:
+            return t
+        with ORDER.issue(negotiated=engine):
+            work = t if t.is_contiguous() else t.contiguous()
+            tr.broadcast_(work, root_rank)
+            if work is not t:
+                t.copy_(work)
+        return t
     if st.size == 1:
         return t
     ring = _ring(t, group, engine)
     if ring is not None:
         return ring.broadcast_(t, root_rank)
     pg = group or group_for(t, engine)
-    if _native_gpu(t) or _gloo_ok(t.dtype):
+    if _gloo_ok(t.dtype):
         if t.is_contiguous():
             dist.broadcast(t, src=root_rank, group=pg)
         else:
@@ -178,25 +256,64 @@ def broadcast_(t: torch.Tensor, root_rank: int, group=None, engine: bool = False
 def alltoall(t: torch.Tensor, splits: Optional[List[int]] = None, group=None,
              engine: bool = False) -> torch.Tensor:
     st = basics.state()
-    if st.size == 1:
+    tr = _gpu_transport(t, group)
+    size = tr.size if tr is not None else st.size
+    if size == 1:
         return t.clone()
-    pg = group or group_for(t, engine)
     n = t.shape[0]
     if splits is None:
-        if n % st.size:
+        if n % size:
             raise ValueError("alltoall: first dim must divide by size when splits is None")
-        splits = [n // st.size] * st.size
-    sp = torch.tensor(splits, dtype=torch.int64, device=t.device)
+        splits = [n // size] * size
+    if len(splits) != size or sum(splits) != n:
+        raise ValueError("alltoall: splits must have one entry per rank summing to dim 0")
+    if tr is not None:
+        with ORDER.issue(negotiated=engine):
+            sp = torch.tensor(splits, dtype=torch.int64, device=t.device)
+            rsp = torch.empty_like(sp)
+            tr.alltoallv(rsp, sp, [1] * size, [1] * size)
+            rsplits = rsp.tolist()
+            out = torch.empty((sum(rsplits),) + tuple(t.shape[1:]), dtype=t.dtype,
+                              device=t.device)
+            tr.alltoallv(out, t.contiguous(), list(splits), rsplits)
+        return out
+    pg = group or group_for(t, engine)
+    sp = torch.tensor(splits, dtype=torch.int64)
     rsp = torch.empty_like(sp)
     dist.all_to_all_single(rsp, sp, group=pg)
     rsplits = rsp.tolist()
-    out = torch.empty((sum(rsplits),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    out = torch.empty((sum(rsplits),) + tuple(t.shape[1:]), dtype=t.dtype)
     dist.all_to_all_single(out, t.contiguous(), rsplits, splits, group=pg)
     return out
 
 
 def barrier(group=None):
+    """Barrier over the world.  On a GPU world the GPU plane takes part too (a
+    1-element allreduce on the current stream, then a stream sync), so every
+    rank's previously enqueued GPU collectives have been issued in order."""
     st = basics.state()
     if st.size == 1:
         return
+    if group is None and st.gpu is not None:
+        with ORDER.issue():
+            st.gpu.barrier(st.device)
+        return
+    if group is None and st.rings:
+        st.rings[0].barrier()
+        return
     dist.barrier(group=group or st.cpu_pg)
+
+
+def max_over_ranks(x: float) -> float:
+    """max of a host float over all ranks (CPU plane; used for timing)."""
+    st = basics.state()
+    if st.size == 1:
+        return float(x)
+    v = allgather(torch.tensor([float(x)], dtype=torch.float64))
+    return float(v.max())
+
+
+def gpu_stats() -> dict:
+    """Cumulative calls / bytes of the GPU transport (empty without one)."""
+    st = basics.state()
+    return st.gpu.stats() if st.gpu is not None else {}

@@ -10,12 +10,19 @@ list of responses (tensors submitted by every rank, validated for matching
 dtype/shape/op/root, fused up to ``HOROVOD_FUSION_THRESHOLD``).  Every rank then
 executes the identical response list, so the RCCL/gloo collectives match.
 
-GPU execution happens on the engine's own high-priority HIP stream: wait on
-each tensor's ready event, one multi-tensor pack kernel (K1, fused compression
-cast + prescale) into the persistent fusion buffer, one RCCL collective, one
-unpack kernel (K2, fused decompress + postscale), done event.  The host never
-waits on the GPU; ``synchronize(handle)`` makes the caller's stream wait on the
-done event.
+GPU execution happens on mivod's high-priority HIP comm stream — the same
+stream and the same RCCL communicator as the static gradient schedule, in the
+cross-rank order of ``order.ORDER`` (each cycle reports this rank's collective
+count; the coordinator answers with the point at which the cycle's GPU
+responses run): wait on each tensor's ready event, one multi-tensor pack kernel
+(K1, fused compression cast + prescale) into the persistent fusion buffer, one
+RCCL collective, one unpack kernel (K2, fused decompress + postscale), done
+event.  The host never waits on the GPU; ``synchronize(handle)`` makes the
+caller's stream wait on the done event.
+
+The request a rank submits carries the *wire* dtype (after compression) and the
+pre-/postscale factors, so the coordinator validates and fuses on what actually
+travels (horovod compresses before enqueueing, which has the same effect).
 """
 from __future__ import annotations
 
@@ -30,6 +37,7 @@ import torch
 from ..ops import kernels as K
 from ..ops.compression import Compression
 from . import collectives as C
+from .order import ORDER
 
 log = logging.getLogger("mivod")
 
@@ -70,10 +78,19 @@ class Handle:
         self.splits = splits
         self.enqueue_time = time.time()
 
+    def wire_dtype(self) -> torch.dtype:
+        t = self.tensor
+        if self.kind != ALLREDUCE or not t.dtype.is_floating_point:
+            return t.dtype
+        return self.compression.wire_dtype(t.dtype)
+
     def request(self, device_index: int):
         t = self.tensor
-        return (self.name, self.kind, _DTYPE_CODE.get(t.dtype, str(t.dtype)), tuple(t.shape),
-                int(self.root), int(self.op), device_index, t.numel() * t.element_size())
+        wd = self.wire_dtype()
+        es = torch.empty((), dtype=wd).element_size()
+        return (self.name, self.kind, _DTYPE_CODE.get(wd, str(wd)), tuple(t.shape),
+                int(self.root), int(self.op), device_index, t.numel() * es,
+                float(self.prescale), float(self.postscale))
 
 
 class LocalController:
@@ -84,9 +101,10 @@ class LocalController:
     def __init__(self, fusion_threshold: int):
         self.fusion_threshold = fusion_threshold
 
-    def negotiate(self, requests, shutdown=False):
-        return fuse_responses([(r[1], [r[0]], "") for r in requests],
-                              {r[0]: r for r in requests}, self.fusion_threshold), shutdown
+    def negotiate(self, requests, shutdown=False, position=0):
+        return (fuse_responses([(r[1], [r[0]], "") for r in requests],
+                               {r[0]: r for r in requests}, self.fusion_threshold),
+                shutdown, position)
 
     def close(self):
         pass
@@ -98,7 +116,8 @@ def fuse_responses(responses, req_by_name, threshold):
         if (out and not err and kind == ALLREDUCE and out[-1][0] == ALLREDUCE and not out[-1][2]):
             prev = out[-1][1]
             r0, r1 = req_by_name[prev[0]], req_by_name[names[0]]
-            same = (r0[2] == r1[2] and r0[5] == r1[5] and r0[6] == r1[6])
+            same = (r0[2] == r1[2] and r0[5] == r1[5] and (r0[6] < 0) == (r1[6] < 0)
+                    and tuple(r0[8:10]) == tuple(r1[8:10]))
             total = sum(req_by_name[n][7] for n in prev) + r1[7]
             if same and total <= threshold and r1[5] != C.Adasum:
                 prev.extend(names)
@@ -128,7 +147,8 @@ class Engine:
     def start(self):
         st = self.st
         if st.device.type == "cuda":
-            self.stream = torch.cuda.Stream(device=st.device, priority=-1)
+            # ONE comm stream for the bucket schedule and the named ops
+            self.stream = st.comm_stream or torch.cuda.Stream(device=st.device, priority=-1)
         from ..utils import timeline as TL
         self.tl = TL.get()
         if st.size == 1:
@@ -167,6 +187,8 @@ class Engine:
                 raise ValueError(f"Duplicate name '{name}' submitted before the previous "
                                  "operation with that name completed")
             self.inflight[name] = h
+            if tensor.is_cuda:
+                ORDER.submitted(1)      # direct GPU collectives wait for its response
             self.pending.append(h)
             self.cv.notify_all()
         if self.tl is not None:
@@ -186,39 +208,58 @@ class Engine:
                 stopping = not self.running
             reqs = [h.request(self.st.device.index if h.tensor.is_cuda else -1) for h in batch]
             self._waiting.update({h.name: h for h in batch})
+            position = ORDER.position()
             try:
-                responses, all_shutdown = self.controller.negotiate(reqs, stopping)
+                responses, all_shutdown, exec_at = self.controller.negotiate(reqs, stopping,
+                                                                             position)
             except Exception as e:  # control plane failure: fail every outstanding op
                 log.error("mivod negotiation failed: %s", e)
                 self._fail_all(HorovodInternalError(str(e)))
                 break
+            gpu_fns, n_gpu = [], 0
             for kind, names, err in responses:
                 hs = [self._waiting.pop(n) for n in names if n in self._waiting]
                 if not hs:
                     continue
+                on_gpu = hs[0].tensor.is_cuda
+                if on_gpu:
+                    n_gpu += len(hs)
                 if err:
                     for h in hs:
                         self._finish(h, error=HorovodInternalError(err))
                     continue
-                try:
-                    self._execute(kind, hs)
-                except Exception as e:
-                    log.exception("mivod collective failed")
-                    for h in hs:
-                        if not h.done.is_set():
-                            self._finish(h, error=HorovodInternalError(repr(e)))
+                if on_gpu:
+                    gpu_fns.append(lambda kind=kind, hs=hs: self._run(kind, hs))
+                else:
+                    self._run(kind, hs)
+            if n_gpu:
+                ORDER.responded(exec_at, n_gpu, gpu_fns)
             if stopping and all_shutdown:
                 self._fail_all(HorovodInternalError("mivod shut down with pending operations"))
                 break
 
+    def _run(self, kind, hs: List[Handle]):
+        try:
+            self._execute(kind, hs)
+        except Exception as e:
+            log.exception("mivod collective failed")
+            for h in hs:
+                if not h.done.is_set():
+                    self._finish(h, error=HorovodInternalError(repr(e)))
+
     def _fail_all(self, err):
+        n_gpu = 0
         for h in list(self._waiting.values()):
+            n_gpu += int(h.tensor.is_cuda)
             self._finish(h, error=err)
         self._waiting = {}
         with self.cv:
             for h in self.pending:
+                n_gpu += int(h.tensor.is_cuda)
                 self._finish(h, error=err)
             self.pending = []
+        if n_gpu:
+            ORDER.responded(ORDER.position(), n_gpu, [])
 
     def _finish(self, h: Handle, error=None):
         h.error = error
@@ -235,6 +276,10 @@ class Engine:
             with torch.cuda.stream(self.stream):
                 for h in hs:
                     self.stream.wait_event(h.ready_event)
+                    # caller-stream allocations used on the comm stream
+                    h.tensor.record_stream(self.stream)
+                    if h.output is not None and h.output.data_ptr() != h.tensor.data_ptr():
+                        h.output.record_stream(self.stream)
                 self._execute_on_stream(kind, hs)
                 for h in hs:
                     h.done_event = torch.cuda.Event()
@@ -256,9 +301,7 @@ class Engine:
         tl = self.tl
         if kind == ALLREDUCE:
             h0 = hs[0]
-            wire = h0.compression.wire_dtype(h0.tensor.dtype)
-            if h0.tensor.dtype.is_floating_point is False:
-                wire = h0.tensor.dtype
+            wire = h0.wire_dtype()
             if len(hs) == 1 and wire == h0.tensor.dtype and h0.prescale == 1.0 and \
                     h0.output is not None and h0.tensor.is_contiguous():
                 out = h0.output
@@ -282,17 +325,19 @@ class Engine:
                 for h in hs: tl.activity(h.name, "MEMCPY_IN_FUSION_BUFFER")
             float_path = h0.tensor.dtype in (torch.float32, torch.float16, torch.bfloat16)
             if float_path:
-                by_dt: Dict[torch.dtype, tuple] = {}
+                # one pack launch per (dtype, prescale): every handle keeps its own factor
+                by_key: Dict[tuple, tuple] = {}
                 for h, o in zip(hs, offs):
                     t = h.tensor if h.tensor.is_contiguous() else h.tensor.contiguous()
-                    e = by_dt.setdefault(t.dtype, ([], [], h.prescale))
+                    e = by_key.setdefault((t.dtype, float(h.prescale)), ([], []))
                     e[0].append(t)
                     e[1].append(o)
-                for t_dt, (ts, os_, pre) in by_dt.items():
+                for (_dt, pre), (ts, os_) in by_key.items():
                     K.pack(ts, buf, os_, scale=pre)
             else:
                 for h, o in zip(hs, offs):
-                    buf[o:o + h.tensor.numel()].copy_(h.tensor.reshape(-1))
+                    v = h.tensor.reshape(-1)
+                    buf[o:o + h.tensor.numel()].copy_(v * h.prescale if h.prescale != 1.0 else v)
             if tl:
                 for h in hs: tl.activity(h.name, _coll_phase(buf))
             table = None

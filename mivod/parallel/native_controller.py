@@ -24,6 +24,7 @@ class NativeController:
         c.stall_check_s = float(cfg.stall_check_time_s)
         c.stall_shutdown_s = float(cfg.stall_shutdown_time_s)
         c.connect_timeout_s = float(os.environ.get("MIVOD_INIT_TIMEOUT_S", "300"))
+        c.cache_capacity = max(0, int(cfg.cache_capacity))
         self.ctl = _mvcore.Controller(c)
         from ..utils import timeline as TL
         tl = TL.get()
@@ -42,8 +43,9 @@ class NativeController:
             host, port = addr.rsplit(":", 1)
             self.ctl.connect(host, int(port))
 
-    def negotiate(self, requests, shutdown=False):
-        return self.ctl.negotiate(list(requests), bool(shutdown))
+    def negotiate(self, requests, shutdown=False, position=0):
+        """-> (responses, all_shutdown, exec_at)"""
+        return self.ctl.negotiate(list(requests), bool(shutdown), int(position))
 
     def last_stalls(self):
         return self.ctl.last_stalls()

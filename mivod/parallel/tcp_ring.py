@@ -59,6 +59,9 @@ class TcpRing:
         nxt = (rank + 1) % size
         host, p = store.get(f"mivod/ring/{tag}/{nxt}").decode().rsplit(":", 1)
         self.ring.connect(host, int(p))
+        io_timeout = float(os.environ.get("HOROVOD_STALL_SHUTDOWN_TIME_SECONDS", "0") or 0)
+        if io_timeout > 0:
+            self.ring.set_timeout(io_timeout)
 
     # ---------------------------------------------------------------- ops
     def allreduce_(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:

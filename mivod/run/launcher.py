@@ -328,7 +328,8 @@ class _Pump(threading.Thread):
 
 
 def launch(slots: List[Slot], command: List[str], extra_env: Dict[str, str],
-           tag_output: bool = False, master_port: int = 0, ssh_port: Optional[int] = None,
+           tag_output: Optional[bool] = None, master_port: int = 0,
+           ssh_port: Optional[int] = None,
            verbose: bool = False, output_dir: Optional[str] = None) -> int:
     size = len(slots)
     first = slots[0].host
@@ -338,7 +339,7 @@ def launch(slots: List[Slot], command: List[str], extra_env: Dict[str, str],
     master_port = master_port or _free_port()
     procs: List[subprocess.Popen] = []
     pumps = []
-    tag = tag_output or size > 1
+    tag = tag_output if tag_output is not None else size > 1   # default: tag when N > 1
     cwd = os.getcwd()
     for s in slots:
         env = dict(os.environ)
@@ -433,7 +434,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         env["NCCL_SOCKET_IFNAME"] = args.network_interface
         env["GLOO_SOCKET_IFNAME"] = args.network_interface
     env.update(exported_env(args.export))
-    return launch(slots, command, env, args.tag_output, args.master_port, args.ssh_port,
+    return launch(slots, command, env, args.tag_output or None, args.master_port, args.ssh_port,
                   args.verbose, args.output_filename)
 
 

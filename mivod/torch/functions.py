@@ -178,6 +178,10 @@ def broadcast_optimizer_state(optimizer, root_rank: int = 0) -> None:
                 if torch.is_tensor(s):
                     a.step = int(s.item())
                     break
+            # the exact fp32 master was just broadcast: keep it.  Without this the
+            # version bump of a preceding broadcast_parameters makes the next step
+            # re-seed the master from the (bf16) model copy on every rank.
+            a.versions = [p._version for p in a.params]
     else:
         optimizer.load_state_dict(state_dict)
     if tensors and tensors[0].is_cuda:

@@ -105,6 +105,9 @@ class GraphedStep:
             raise ValueError("make_graphed_step needs at least one eager warmup step")
         self.dist = isinstance(optimizer, _DistributedOptimizerMixin)
         if self.dist:
+            if getattr(optimizer, "_mvd_guard", False):
+                raise ValueError("make_graphed_step: the fp16-wire overflow guard reads its flag "
+                                 "on the host between steps; pass overflow_guard=False")
             if optimizer._mvd_bpps != 1:
                 raise ValueError("graph mode needs backward_passes_per_step == 1")
             optimizer._mvd_autotune = None         # the captured bucket plan is final

@@ -26,6 +26,16 @@ MI355X design (not a translation of horovod's per-tensor async ops):
   whole update overlaps the remaining backward; ``step()`` is then only a
   stream wait.  Plain torch optimizers get zero-copy gradient views into the
   reduced bucket instead.
+* **Overflow guard** (default with fp16 wire compression): the pack kernel
+  flags non-finite values (bf16 gradients above the fp16 range included), one
+  4-byte MAX-allreduce makes the flag identical on every rank, and the fused
+  update kernels read it on the device and skip the step — every rank skips
+  identically, with no host sync.  ``grad_scale="dynamic"`` additionally
+  scales the wire by s (halved after an overflow, doubled back after
+  ``MIVOD_GUARD_GROWTH_STEPS`` clean steps, capped at 1) and folds 1/s into the
+  update.
+* **Timeline**: with ``HOROVOD_TIMELINE`` set, every bucket's pack / collective
+  / fused step is recorded with GPU timestamps (``utils.timeline.PhaseRecorder``).
 """
 from __future__ import annotations
 
@@ -43,6 +53,8 @@ from ..optim.fused import Arena, FusedOptimizer, _align
 from ..parallel import collectives as C
 from ..utils import markers as MK
 from ..utils import timeline as TL
+
+_log = __import__("logging").getLogger("mivod")
 
 
 class _GradArena:
@@ -161,12 +173,18 @@ class _DistributedOptimizerMixin:
 
     # ------------------------------------------------------------------ setup
     def _mvd_setup(self, named_parameters, compression, backward_passes_per_step, op,
-                   bucket_mb, first_bucket_mb, gradient_predivide_factor):
+                   bucket_mb, first_bucket_mb, gradient_predivide_factor,
+                   overflow_guard=None, grad_scale=None):
         st = basics.state()
         if not st.initialized:
             raise ValueError(basics._NOT_INIT)
         cfg = st.config
+        if compression is None:
+            compression = Compression.by_name(cfg.compression)   # MIVOD_COMPRESSION
         self._mvd_size = st.size
+        # collectives run when there are peers, or on the 1-rank RCCL comm that
+        # MIVOD_FORCE_COLLECTIVES=1 builds (exercises the GPU path on one GPU)
+        self._mvd_comm = st.size > 1 or st.gpu is not None
         self._mvd_rank = st.rank
         self._mvd_compression = compression
         self._mvd_bpps = int(backward_passes_per_step)
@@ -236,6 +254,26 @@ class _DistributedOptimizerMixin:
         self._mvd_done_event = None
         self._mvd_nonfinite = None
         self._mvd_steps = 0
+        # overflow guard (fp16 wire by default; MIVOD_OVERFLOW_GUARD=0/1 overrides)
+        import os
+        env_guard = os.environ.get("MIVOD_OVERFLOW_GUARD", "")
+        if overflow_guard is None:
+            overflow_guard = (env_guard == "1") if env_guard else (wire(torch.bfloat16)
+                                                                     == torch.float16)
+        self._mvd_guard = bool(overflow_guard) and self._mvd_fused
+        if bool(overflow_guard) and not self._mvd_fused:
+            warnings.warn("mivod overflow guard needs a mivod.optim.Fused* optimizer; disabled")
+        self._mvd_dynamic = self._mvd_guard and (grad_scale == "dynamic" or
+                                                 os.environ.get("MIVOD_GRAD_SCALE", "") ==
+                                                 "dynamic")
+        self._mvd_gs = float(grad_scale) if isinstance(grad_scale, (int, float)) else 1.0
+        self._mvd_gs_growth = int(os.environ.get("MIVOD_GUARD_GROWTH_STEPS", "200"))
+        self._mvd_gs_good = 0
+        self._mvd_flag = None             # device int32 non-finite flag of the step
+        self._mvd_flag_host = None        # pinned copy + event of the previous step's flag
+        self._mvd_flag_ev = None
+        self._mvd_skipped = 0
+        self._mvd_rec = None
         self._mvd_autotune = None
         if cfg.autotune and bucket_mb is None and first_bucket_mb is None:
             from ..parallel.autotune import BucketAutotuner
@@ -257,7 +295,7 @@ class _DistributedOptimizerMixin:
         import hashlib
         h = hashlib.blake2b(digest_size=8)
         h.update(repr((C.op_name(self._mvd_op), self._mvd_compression.__name__,
-                       self._mvd_bpps)).encode())
+                       self._mvd_bpps, self._mvd_guard, self._mvd_gs)).encode())
         for b in self._mvd_buckets:
             h.update(repr((str(b.arena.grad.dtype), b.hi - b.lo,
                            [(self._mvd_names[id(p)], tuple(p.shape)) for p in b.params])).encode())
@@ -291,15 +329,58 @@ class _DistributedOptimizerMixin:
             self._mvd_launch(bs[self._mvd_next])
             self._mvd_next += 1
 
+    def _mvd_guard_begin(self, device):
+        """Step start (guard on): consume the previous step's flag — read at the
+        same step on every rank (the wait is for a flag allreduced at the end of
+        the previous step, long done by now), adjust the dynamic scale, reset."""
+        if self._mvd_flag_ev is not None:
+            self._mvd_flag_ev.synchronize()
+            if int(self._mvd_flag_host[0]) != 0:
+                self._mvd_skipped += 1
+                if self._mvd_fused:
+                    for a in self._mvd_arenas:
+                        a.step = max(a.step - 1, 0)   # the skipped update did not count
+                msg = (f"mivod: non-finite gradients on the fp16 wire (or in the gradients) — "
+                       f"optimizer step {self._mvd_steps} skipped on every rank")
+                if self._mvd_dynamic:
+                    self._mvd_gs = max(self._mvd_gs * 0.5, 2.0 ** -24)
+                    msg += f"; wire scale -> {self._mvd_gs:g}"
+                    self._mvd_gs_good = 0
+                _log.warning(msg)
+                warnings.warn(msg)
+            elif self._mvd_dynamic:
+                self._mvd_gs_good += 1
+                if self._mvd_gs_good >= self._mvd_gs_growth and self._mvd_gs < 1.0:
+                    self._mvd_gs = min(self._mvd_gs * 2.0, 1.0)
+                    self._mvd_gs_good = 0
+            self._mvd_flag_ev = None
+        if self._mvd_flag is None:
+            self._mvd_flag = torch.zeros(1, dtype=torch.int32, device=device)
+            if device.type == "cuda":
+                self._mvd_flag_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            else:
+                self._mvd_flag_host = torch.zeros(1, dtype=torch.int32)
+        else:
+            self._mvd_flag.zero_()
+
     def _mvd_launch(self, b: _Bucket):
+        a = b.arena
         if not self._mvd_in_step:
             self._mvd_in_step = True
+            self._mvd_rec = TL.recorder()
+            if self._mvd_guard:
+                self._mvd_guard_begin(a.grad.device)
             if self._mvd_fused:
                 self._mv_begin_step()
-        a = b.arena
         size = self._mvd_size
         prescale = 1.0 / self._mvd_predivide if self._mvd_op == C.Average else 1.0
+        prescale *= self._mvd_gs
+        flag = self._mvd_flag if self._mvd_guard else None
+        rec = self._mvd_rec
+        t_pack = rec.event() if rec is not None and a.grad.is_cuda else (
+            rec.host() if rec is not None else None)
         groups: Dict[torch.dtype, tuple] = {}
+        scan_inplace = False
         with torch.no_grad():
             for k, p in enumerate(b.params):
                 i = b.i0 + k
@@ -314,6 +395,7 @@ class _DistributedOptimizerMixin:
                         g.dtype == a.grad.dtype and g.stride() == p.stride():
                     if prescale != 1.0:
                         g.mul_(prescale)
+                    scan_inplace = flag is not None
                     continue  # gradient already lives in its bucket slot (accumulated in place)
                 if g.stride() != p.stride() or not K.is_dense(g):
                     g = torch.empty_like(p, dtype=g.dtype).copy_(g)
@@ -322,7 +404,10 @@ class _DistributedOptimizerMixin:
                 ent[1].append(lo)
             with MK.range(f"mivod.pack.{b.name}"):
                 for dt, (gl, ol) in groups.items():
-                    K.pack(gl, a.grad, ol, scale=prescale)
+                    K.pack(gl, a.grad, ol, scale=prescale, nonfinite=flag)
+                if scan_inplace:      # zero-copy grads are scanned in place
+                    seg = a.grad[b.lo:b.hi]
+                    K.flat_cast(seg, seg, 1.0, flag)
             if self._mvd_fused:
                 for p in b.params:
                     p.grad = None            # freed on the compute stream after the pack
@@ -332,6 +417,10 @@ class _DistributedOptimizerMixin:
         # DAG ~15 us/kernel slower than one chain (scripts/debug/graph_speed.py), and
         # with one rank there is no RCCL to overlap
         cuda = flat.is_cuda and self._mvd_stream is not None and not self._mvd_inline
+        t_packed = None
+        if rec is not None:
+            t_packed = rec.event() if flat.is_cuda else rec.host()
+            rec.add(b.name, "MEMCPY_IN_FUSION_BUFFER", t_pack, t_packed)
         if cuda:
             ev = torch.cuda.Event()
             ev.record()
@@ -341,7 +430,8 @@ class _DistributedOptimizerMixin:
         with ctx:
             if cuda:
                 self._mvd_stream.wait_event(ev)
-            if size > 1:
+            if self._mvd_comm:
+                t0 = (rec.event() if cuda else rec.host()) if rec is not None else None
                 with MK.range(f"mivod.allreduce.{b.name}"):
                     if self._mvd_op == C.Adasum:
                         C.allreduce_(flat, C.Adasum, adasum_table=a.table(b.i0, b.i1))
@@ -349,22 +439,72 @@ class _DistributedOptimizerMixin:
                         C.allreduce_(flat, C.Sum)
                     else:
                         C.allreduce_(flat, C.Average if self._mvd_op == C.Average else C.Sum)
+                if rec is not None:
+                    phase = "ADASUM" if self._mvd_op == C.Adasum else (
+                        "NCCL_ALLREDUCE" if cuda else "RING_ALLREDUCE")
+                    rec.add(b.name, phase, t0, rec.event() if cuda else rec.host())
             if self._mvd_fused:
-                gscale = 1.0
-                if self._mvd_op == C.Average:
-                    gscale = self._mvd_predivide / size
-                with MK.range(f"mivod.step.{b.name}"):
-                    self._mv_apply(a, b.i0, b.i1, gscale)
+                if not self._mvd_guard:
+                    self._mvd_apply_bucket(b, cuda)
             else:
                 post = self._mvd_predivide if (self._mvd_op == C.Average and size > 1) else 1.0
+                t0 = (rec.event() if cuda else rec.host()) if rec is not None else None
                 if post != 1.0:
                     flat.mul_(post)
                 self._mvd_expose_grads(b)
+                if rec is not None:
+                    rec.add(b.name, "MEMCPY_OUT_FUSION_BUFFER", t0,
+                            rec.event() if cuda else rec.host())
             if cuda:
                 ev2 = torch.cuda.Event()
                 ev2.record()
                 self._mvd_done_event = ev2
         b.launched = True
+
+    def _mvd_apply_bucket(self, b: _Bucket, cuda: bool):
+        """The fused optimizer step of one reduced bucket (current stream)."""
+        rec = self._mvd_rec
+        gscale = 1.0 / self._mvd_gs
+        if self._mvd_op == C.Average:
+            gscale *= self._mvd_predivide / self._mvd_size
+        t0 = (rec.event() if cuda else rec.host()) if rec is not None else None
+        self._mv_skip = self._mvd_flag if self._mvd_guard else None
+        with MK.range(f"mivod.step.{b.name}"):
+            self._mv_apply(b.arena, b.i0, b.i1, gscale)
+        self._mv_skip = None
+        if rec is not None:
+            rec.add(b.name, "OPTIMIZER_STEP", t0, rec.event() if cuda else rec.host())
+
+    def _mvd_guard_finish(self):
+        """synchronize() with the guard on: OR the flag across ranks (one 4-byte
+        MAX allreduce), then run every bucket's fused step with the device skip
+        flag, on the comm stream after the last bucket's collective."""
+        flag = self._mvd_flag
+        if flag is None:
+            return
+        cuda = flag.is_cuda and self._mvd_stream is not None and not self._mvd_inline
+        ctx = torch.cuda.stream(self._mvd_stream) if cuda else contextlib.nullcontext()
+        with ctx:
+            if self._mvd_comm:
+                C.allreduce_(flag, C.Max)
+            for b in self._mvd_buckets:
+                self._mvd_apply_bucket(b, cuda)
+            if flag.is_cuda:
+                self._mvd_flag_host.copy_(flag, non_blocking=True)
+                self._mvd_flag_ev = torch.cuda.Event()
+                self._mvd_flag_ev.record()
+            else:
+                self._mvd_flag_host.copy_(flag)
+                self._mvd_flag_ev = _DoneEvent()
+            if cuda:
+                ev2 = torch.cuda.Event()
+                ev2.record()
+                self._mvd_done_event = ev2
+
+    def guard_stats(self) -> dict:
+        """Overflow-guard counters (skipped steps so far, current wire scale)."""
+        return {"enabled": self._mvd_guard, "skipped_steps": self._mvd_skipped,
+                "wire_scale": self._mvd_gs, "dynamic": self._mvd_dynamic}
 
     def _mvd_expose_grads(self, b: _Bucket):
         """Plain optimizers: p.grad := reduced values (zero-copy view when the
@@ -387,13 +527,14 @@ class _DistributedOptimizerMixin:
     # -------------------------------------------------------------- user API
     def synchronize(self):
         with self._mvd_lock:
-            if any(c != self._mvd_bpps for c in self._mvd_counts.values()) and \
-                    self._mvd_counts and self._mvd_bpps > 1:
-                pass  # partial accumulation windows are allowed; missing grads reduce as zeros
+            # buckets not launched by the hooks (unused parameters, a partial
+            # backward_passes_per_step window) reduce now, missing grads as zeros
             for b in self._mvd_buckets:
                 if not b.launched:
                     b.pending = 0
             self._mvd_launch_ready()
+            if self._mvd_guard and self._mvd_in_step:
+                self._mvd_guard_finish()
             if self._mvd_stream is not None and torch.cuda.is_available() and \
                     not self._mvd_inline:
                 torch.cuda.current_stream().wait_stream(self._mvd_stream)
@@ -474,10 +615,20 @@ class _DistributedOptimizerMixin:
                 for b in self._mvd_buckets]
 
 
-def DistributedOptimizer(optimizer, named_parameters=None, compression=Compression.none,
+class _DoneEvent:
+    def synchronize(self):
+        pass
+
+
+def DistributedOptimizer(optimizer, named_parameters=None, compression=None,
                          backward_passes_per_step: int = 1, op=C.Average, bucket_mb=None,
-                         first_bucket_mb=None, gradient_predivide_factor: float = 1.0):
+                         first_bucket_mb=None, gradient_predivide_factor: float = 1.0,
+                         overflow_guard=None, grad_scale=None):
     """Wrap ``optimizer`` so gradients are averaged (``op``) across all ranks.
+
+    ``compression`` defaults to ``MIVOD_COMPRESSION`` (``none``).  With an fp16
+    wire the overflow guard is on unless ``overflow_guard=False``;
+    ``grad_scale="dynamic"`` (or a float) scales the wire (see module doc).
 
     Returns an instance of a dynamically created subclass of the optimizer's
     class (same class name, so ``isinstance`` and pickled configs keep working),
@@ -490,5 +641,5 @@ def DistributedOptimizer(optimizer, named_parameters=None, compression=Compressi
     obj = cls.__new__(cls)
     obj.__dict__.update(optimizer.__dict__)
     obj._mvd_setup(named_parameters, compression, backward_passes_per_step, op, bucket_mb,
-                   first_bucket_mb, gradient_predivide_factor)
+                   first_bucket_mb, gradient_predivide_factor, overflow_guard, grad_scale)
     return obj

@@ -52,7 +52,7 @@ def save_checkpoint(path: str, model: torch.nn.Module, optimizer=None, epoch: Op
         return None
     from safetensors.torch import save_file
     tensors = {f"model.{k}": v.detach().contiguous().cpu() for k, v in model.state_dict().items()}
-    meta = {"format": "mivod.checkpoint/1", "epoch": json.dumps(epoch),
+    meta = {"format": _FORMAT, "epoch": json.dumps(epoch),
             "extra": json.dumps(extra or {})}
     if optimizer is not None:
         ot, osc, groups = _flatten_optimizer(optimizer)
@@ -108,18 +108,34 @@ def load_checkpoint(path: str, model: torch.nn.Module, optimizer=None, broadcast
     return info
 
 
-_CKPT_RE = re.compile(r"checkpoint-(\d+)\.(safetensors|h5|pt)$")
+_CKPT_RE = re.compile(r"checkpoint-(\d+)\.safetensors$")
+_FORMAT = "mivod.checkpoint/1"
+
+
+def _is_mivod_checkpoint(path: str) -> bool:
+    """Only files this module wrote (safetensors with our format tag) — Keras
+    ``checkpoint-{epoch}.h5`` files or foreign files in the same directory are
+    never picked up by resume."""
+    try:
+        from safetensors import safe_open
+        with safe_open(path, framework="pt") as f:
+            return (f.metadata() or {}).get("format") == _FORMAT
+    except Exception:
+        return False
 
 
 def latest_checkpoint(directory: str) -> Optional[str]:
     if not os.path.isdir(directory):
         return None
-    best, path = -1, None
+    cands = []
     for f in os.listdir(directory):
         m = _CKPT_RE.search(f)
-        if m and int(m.group(1)) > best:
-            best, path = int(m.group(1)), os.path.join(directory, f)
-    return path
+        if m:
+            cands.append((int(m.group(1)), os.path.join(directory, f)))
+    for _ep, path in sorted(cands, reverse=True):
+        if _is_mivod_checkpoint(path):
+            return path
+    return None
 
 
 def resume_from(directory: str, model, optimizer=None) -> int:

@@ -3,8 +3,13 @@
 ``MIVOD_FAULT="<rank>:<step>:<kind>[,...]"`` makes rank <rank> misbehave when
 its DistributedOptimizer finishes step <step> (1-based):
 ``crash`` (exit 17 without cleanup), ``hang`` (sleep forever), ``raise``
-(RuntimeError).  Used to check that the launcher tears the job down and that
-the stall inspector / RCCL watchdog report instead of hanging silently.
+(RuntimeError).  Used to check that the job ends instead of hanging: the
+launcher tears every rank down when one exits non-zero; with
+``HOROVOD_STALL_SHUTDOWN_TIME_SECONDS`` set, the surviving ranks' collectives
+time out — the CPU ring's per-step I/O timeout, and on GPU the RCCL watchdog
+thread of ``mivod._mvcomm`` (csrc/comm/comm.cc: ncclCommGetAsyncError polling +
+ncclCommAbort of a collective older than the limit) — so they exit non-zero
+and the launcher reaps the hung rank (tests/test_checkpoint_faults_autotune.py).
 """
 from __future__ import annotations
 

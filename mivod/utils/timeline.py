@@ -75,6 +75,14 @@ class _PyTimeline:
             self._w({"name": what, "ph": "i", "pid": self._pid(name), "tid": 1, "ts": self._ts(),
                      "s": "p"})
 
+    def complete(self, name, phase, ts_us, dur_us):
+        with self.lock:
+            self._w({"name": phase, "ph": "X", "pid": self._pid(name), "tid": 2, "ts": int(ts_us),
+                     "dur": max(0, int(dur_us))})
+
+    def now_us(self):
+        return self._ts()
+
     def mark_cycle(self):
         if self.mark_cycles:
             self.instant("cycle", "CYCLE_START")
@@ -106,8 +114,11 @@ def start_timeline(path: str, mark_cycles: bool = False):
 
 
 def stop_timeline():
-    global _TL
+    global _TL, _REC
     with _LOCK:
+        if _REC is not None:
+            _REC.stop()
+            _REC = None
         if _TL is not None:
             _TL.close()
             _TL = None
@@ -130,3 +141,105 @@ def note_plan(buckets):
         return
     for b in buckets:
         tl.instant(b.name, f"PLAN {b.nbytes} bytes, {len(b.params)} tensors")
+
+
+# ---------------------------------------------------------------------------
+# GPU phases of the static gradient schedule
+# ---------------------------------------------------------------------------
+_REC = None
+
+
+class PhaseRecorder:
+    """Turns (start, end) timing-event pairs recorded on the compute / comm
+    streams into timeline "X" events with GPU timestamps: per bucket
+    ``MEMCPY_IN_FUSION_BUFFER`` (pack), ``NCCL_ALLREDUCE`` / ``ADASUM`` (the
+    collective), ``OPTIMIZER_STEP`` (fused update) or ``MEMCPY_OUT_FUSION_BUFFER``.
+    A daemon thread polls the end events, so the hot path never waits; on CPU
+    tensors the phases are timed on the host."""
+
+    def __init__(self, tl):
+        self.tl = tl
+        self.items = []
+        self.lock = threading.Lock()
+        self.cv = threading.Condition(self.lock)
+        self.ref = None          # (cuda event, timeline us at that event)
+        self.running = True
+        self.thread = threading.Thread(target=self._run, name="mivod-timeline-gpu", daemon=True)
+        self.thread.start()
+
+    def _ref(self):
+        import torch
+        if self.ref is None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            ev.synchronize()
+            self.ref = (ev, self.tl.now_us())
+        return self.ref
+
+    def event(self):
+        """A timing event recorded now on the current stream (None on CPU)."""
+        import torch
+        if not torch.cuda.is_available():
+            return None
+        self._ref()
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def host(self):
+        return self.tl.now_us()
+
+    def add(self, name: str, phase: str, start, end):
+        if start is None or end is None:
+            return
+        if isinstance(start, (int, float)):
+            self.tl.complete(name, phase, int(start), int(end - start))
+            return
+        with self.cv:
+            self.items.append((name, phase, start, end))
+            self.cv.notify()
+
+    def _run(self):
+        while True:
+            with self.cv:
+                while self.running and not self.items:
+                    self.cv.wait(0.05)
+                if not self.running and not self.items:
+                    return
+                items, self.items = self.items, []
+            keep = []
+            for it in items:
+                name, phase, s, e = it
+                try:
+                    if not e.query():
+                        keep.append(it)
+                        continue
+                    ref_ev, ref_us = self.ref
+                    ts = ref_us + ref_ev.elapsed_time(s) * 1000.0
+                    dur = s.elapsed_time(e) * 1000.0
+                    self.tl.complete(name, phase, int(ts), int(dur))
+                except Exception:
+                    pass
+            if keep:
+                with self.cv:
+                    self.items = keep + self.items
+                time.sleep(0.002)
+
+    def stop(self):
+        with self.cv:
+            self.running = False
+            self.cv.notify()
+        self.thread.join(timeout=10)
+
+
+def recorder() -> Optional[PhaseRecorder]:
+    """The GPU phase recorder when a timeline is active on this rank (else None)."""
+    global _REC
+    tl = get()
+    if tl is None:
+        return None
+    if _REC is None:
+        with _LOCK:
+            if _REC is None:
+                _REC = PhaseRecorder(tl)
+    return _REC

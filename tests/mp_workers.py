@@ -617,6 +617,354 @@ def tensorflow_api():
     htf.shutdown()
     print("OK", r)
 
+def adasum_vhdd():
+    """Vector-halving / distance-doubling Adasum (mivod.parallel.adasum) on a fused
+    multi-tensor buffer equals the full-vector recursive-doubling reference within
+    fp32 tolerance, sends <= 2*S*(N-1)/N bytes per rank, and leaves every rank with
+    identical bits — fp32 and bf16 wires, odd segment sizes."""
+    from mivod.ops import kernels as K
+    from mivod.parallel import adasum as A
+    from mivod.parallel import collectives as C
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    sizes = [1, 63, 4096 + 5, 130, 9000, 7]
+    offs, o = [], 0
+    for sz in sizes:
+        offs.append(o)
+        o += (sz + 63) // 64 * 64
+    S = o
+    table = K.make_chunk_table(sizes, "cpu", offs)
+    vecs = []
+    for rr in range(n):
+        v = torch.zeros(S)
+        g = torch.Generator().manual_seed(31 + rr)
+        for sz, off in zip(sizes, offs):
+            v[off:off + sz] = torch.randn(sz, generator=g) * (1 + rr)
+        vecs.append(v)
+    ref = A.adasum_reference(vecs, table)
+    for dt, tol in ((torch.float32, 2e-5), (torch.bfloat16, 3e-2)):
+        buf = vecs[r].to(dt).clone()
+        C.allreduce_(buf, C.Adasum, adasum_table=table)
+        es = buf.element_size()
+        bound = 2 * S * (n - 1) / n * es + 2 * A.LAST["levels"] * A.ALIGN * es
+        assert A.LAST["exchange_bytes"] <= bound, (A.LAST, bound)
+        wire_ref = A.adasum_reference([v.to(dt).float() for v in vecs], table)
+        err = (buf.float() - wire_ref).abs().max().item()
+        scale = wire_ref.abs().max().item()
+        assert err <= tol * scale, (dt, err, scale)
+        if dt == torch.float32:
+            torch.testing.assert_close(buf, ref, rtol=2e-5, atol=2e-5 * scale)
+        allb = C.allgather(buf.float().unsqueeze(0))
+        assert all(torch.equal(allb[0], allb[i]) for i in range(n)), dt
+    # identical inputs: adasum(g, ..., g) = g ; orthogonal inputs: the sum
+    g = torch.linspace(-1, 1, 300)
+    t1 = K.make_chunk_table([300], "cpu")
+    x = g.clone()
+    C.allreduce_(x, C.Adasum, adasum_table=t1)
+    _close(x, g)
+    e = torch.zeros(n * 64)
+    e[r * 64:(r + 1) * 64] = 1.0
+    C.allreduce_(e, C.Adasum, adasum_table=K.make_chunk_table([n * 64], "cpu"))
+    _close(e, torch.ones(n * 64))
+    hvd.shutdown()
+    print("OK", r)
+
+
+def overflow_guard():
+    """fp16 wire + FusedSGD: rank 1 injects inf into one gradient at step 2; the
+    pack kernel flags it, the MAX-allreduced flag makes EVERY rank skip that step
+    (parameters identical across ranks and unchanged by the step), a warning is
+    logged, and training continues afterwards."""
+    import warnings
+    from mivod.optim import FusedSGD
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    torch.manual_seed(0)
+    m = _toy(0)
+    opt = hvd.DistributedOptimizer(FusedSGD(m.parameters(), lr=0.1, momentum=0.9),
+                                   named_parameters=m.named_parameters(),
+                                   compression=hvd.Compression.fp16,
+                                   bucket_mb=0.005, first_bucket_mb=0.001)
+    assert opt.guard_stats()["enabled"]
+    g = torch.Generator().manual_seed(100 + r)
+    x, y = torch.randn(4, 3, 8, 8, generator=g), torch.randint(0, 10, (4,), generator=g)
+    snap = {}
+    inject = [False]
+
+    def poison(gr):               # the fused path frees p.grad after packing: poison
+        if inject[0]:             # the gradient on its way into the accumulator
+            gr = gr.clone()
+            gr.view(-1)[0] = float("inf")
+        return gr
+
+    next(iter(m.parameters())).register_hook(poison)
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        for step in range(1, 5):
+            inject[0] = step == 2 and r == 1
+            before = [p.detach().clone() for p in m.parameters()]
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            opt.step()
+            snap[step] = (before, [p.detach().clone() for p in m.parameters()])
+    b2, a2 = snap[2]
+    assert all(torch.equal(p, q) for p, q in zip(b2, a2)), "overflow step was not skipped"
+    b3, a3 = snap[3]
+    assert any(not torch.equal(p, q) for p, q in zip(b3, a3)), "training did not resume"
+    assert opt.guard_stats()["skipped_steps"] == 1, opt.guard_stats()
+    assert any("skipped on every rank" in str(w.message) for w in caught)
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    allf = hvd.allgather(flat.unsqueeze(0))
+    assert torch.isfinite(allf).all() and torch.equal(allf[0], allf[-1])
+    hvd.shutdown()
+    print("OK", r)
+
+
+def timeline_buckets():
+    """HOROVOD_TIMELINE records every bucket of the static gradient schedule with
+    its pack / collective / fused-step phases as complete events."""
+    import json
+    from mivod.optim import FusedSGD
+    path = os.environ["HOROVOD_TIMELINE"]
+    hvd.init()
+    r = hvd.rank()
+    m = _toy(0)
+    opt = hvd.DistributedOptimizer(FusedSGD(m.parameters(), lr=0.1, momentum=0.9),
+                                   named_parameters=m.named_parameters(),
+                                   bucket_mb=0.005, first_bucket_mb=0.001)
+    nb = len(opt.bucket_plan())
+    assert nb > 1
+    g = torch.Generator().manual_seed(r)
+    x, y = torch.randn(4, 3, 8, 8, generator=g), torch.randint(0, 10, (4,), generator=g)
+    for _ in range(2):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+    hvd.shutdown()
+    from mivod.utils import timeline as TL
+    TL.stop_timeline()
+    if r == 0:
+        ev = json.load(open(path))
+        rows = {e["pid"]: e["args"]["name"] for e in ev if e.get("name") == "process_name"}
+        per = {}
+        for e in ev:
+            if e.get("ph") == "X":
+                per.setdefault(rows[e["pid"]], []).append(e["name"])
+                assert e["dur"] >= 0 and e["ts"] >= 0
+        for k in range(nb):
+            phases = per.get(f"bucket.{k}", [])
+            for ph in ("MEMCPY_IN_FUSION_BUFFER", "RING_ALLREDUCE", "OPTIMIZER_STEP"):
+                assert phases.count(ph) == 2, (k, ph, phases)
+    print("OK", r)
+
+
+def prescale_fusion():
+    """Two allreduces with different prescale factors submitted in one cycle are
+    never fused under one factor (the coordinator keys fusion on them); equal
+    factors fuse; mismatched factors across ranks raise on every rank."""
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    a = torch.full((5,), float(r + 1))
+    b = torch.full((7,), float(r + 1))
+    ha = hvd.allreduce_async(a, name="ps.a", op=hvd.Sum, prescale_factor=0.5)
+    hb = hvd.allreduce_async(b, name="ps.b", op=hvd.Sum, prescale_factor=2.0, postscale_factor=3.0)
+    tot = n * (n + 1) / 2
+    _close(hvd.synchronize(ha), torch.full((5,), 0.5 * tot))
+    _close(hvd.synchronize(hb), torch.full((7,), 6.0 * tot))
+    hs = [hvd.allreduce_async(torch.full((3,), float(r)), name=f"ps.eq{i}", op=hvd.Sum,
+                              prescale_factor=0.25) for i in range(3)]
+    for h in hs:
+        _close(hvd.synchronize(h), torch.full((3,), 0.25 * sum(range(n))))
+    try:
+        hvd.allreduce(torch.ones(2), name="ps.bad", op=hvd.Sum, prescale_factor=1.0 + r)
+    except Exception as e:
+        assert "prescale" in str(e), e
+    else:
+        raise AssertionError("mismatched prescale not detected")
+    hvd.shutdown()
+    print("OK", r)
+
+
+def cache_capacity():
+    """HOROVOD_CACHE_CAPACITY bounds the response cache (FIFO slots, mirrored on
+    the coordinator); all-hit cycles travel as bit vectors; 0 disables the cache.
+    Results stay correct throughout."""
+    from mivod.common import basics as B
+    cap = int(os.environ["HOROVOD_CACHE_CAPACITY"])
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    for it in range(12):
+        names = [f"cc.{(it + k) % 6}" for k in range(3)]
+        hs = [hvd.allreduce_async(torch.full((4,), float(r + k)), name=nm, op=hvd.Sum)
+              for k, nm in enumerate(names)]
+        for k, h in enumerate(hs):
+            _close(hvd.synchronize(h), torch.full((4,), float(sum(range(n)) + n * k)))
+    # a burst of repeated names submitted together -> all-hit cycles
+    for it in range(20):
+        hs = [hvd.allreduce_async(torch.ones(2), name=f"bv.{k}", op=hvd.Sum) for k in range(12)]
+        for h in hs:
+            _close(hvd.synchronize(h), torch.full((2,), float(n)))
+    ctl = B.state().engine.controller.ctl
+    assert ctl.cache_size <= cap, (ctl.cache_size, cap)
+    if cap == 0:
+        assert ctl.cache_size == 0 and ctl.cache_hits == 0
+    if r == 0 and cap >= 12:
+        assert ctl.cache_hits > 0
+    hvd.shutdown()
+    print("OK", r)
+
+
+def ckpt_bf16_resume():
+    """Resume of a bf16 model with a fused optimizer keeps the checkpointed fp32
+    master weights bit-for-bit on every rank (broadcast_parameters followed by
+    broadcast_optimizer_state must not re-seed the master from the bf16 copy)."""
+    import tempfile
+    from mivod.optim import FusedAdam
+    from mivod.utils.checkpoint import load_checkpoint, save_checkpoint
+    hvd.init()
+    r = hvd.rank()
+    d = os.environ.get("MIVOD_TEST_DIR") or tempfile.mkdtemp()
+    path = os.path.join(d, "checkpoint-3.safetensors")
+
+    def make(seed):
+        torch.manual_seed(seed)
+        m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Linear(5, 3)).to(torch.bfloat16)
+        o = hvd.DistributedOptimizer(FusedAdam(m.parameters(), lr=1e-2),
+                                     named_parameters=m.named_parameters())
+        return m, o
+
+    m, o = make(0)
+    hvd.broadcast_parameters(m.state_dict(), 0)
+    x = torch.randn(4, 6, generator=torch.Generator().manual_seed(r)).to(torch.bfloat16)
+    for _ in range(3):
+        o.zero_grad()
+        m(x).float().pow(2).mean().backward()
+        o.step()
+    master = torch.cat([a.master.clone() for a in o._mv_arenas])
+    save_checkpoint(path, m, o, epoch=3)
+    hvd.allreduce(torch.zeros(1), name="ck.barrier")
+    m2, o2 = make(100 + r)                            # different weights per rank
+    info = load_checkpoint(path, m2, o2)
+    assert info["epoch"] == 3
+    o2._mv_begin_step()                               # what the next step does first
+    got = torch.cat([a.master.clone() for a in o2._mv_arenas])
+    assert torch.equal(got, master), (got - master).abs().max()
+    allm = hvd.allgather(got.unsqueeze(0))
+    assert torch.equal(allm[0], allm[-1])
+    hvd.shutdown()
+    print("OK", r)
+
+
+def fault_run():
+    """Training loop for the fault-injection tests (MIVOD_FAULT set by the test)."""
+    from mivod.optim import FusedSGD
+    hvd.init()
+    m = _toy(0)
+    opt = hvd.DistributedOptimizer(FusedSGD(m.parameters(), lr=0.01),
+                                   named_parameters=m.named_parameters())
+    x, y = torch.randn(4, 3, 8, 8), torch.randint(0, 10, (4,))
+    for _ in range(6):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+    hvd.shutdown()
+    print("OK", hvd_rank())
+
+
+def gpu_order():
+    """ONE communicator, two producers: the hook-driven bucket schedule and named
+    ops submitted (a) from a backward hook in the middle of backward and (b) between
+    backward and step (metric averaging) — every rank runs them in the same order,
+    results match the reference and ranks stay bit-identical (2 ranks on one GPU,
+    gloo-gpu wire; the same protocol orders RCCL on 8 GPUs)."""
+    from mivod.optim import FusedSGD
+    from mivod.parallel.order import ORDER
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    dev = hvd.device()
+    assert ORDER.enabled
+    torch.manual_seed(0)
+    m = _toy(0).to(dev)
+    opt = hvd.DistributedOptimizer(FusedSGD(m.parameters(), lr=0.05, momentum=0.9),
+                                   named_parameters=m.named_parameters(),
+                                   bucket_mb=0.002, first_bucket_mb=0.001)
+    assert len(opt.bucket_plan()) >= 3
+    seen = []
+
+    def hook(mod, gin, gout):
+        v = hvd.allreduce(torch.full((3,), float(r + 1), device=dev), name=f"mid.{len(seen)}")
+        seen.append(v)
+
+    bn = [mm for mm in m.modules() if isinstance(mm, torch.nn.BatchNorm2d)][0]
+    bn.register_full_backward_hook(hook)           # fires in the middle of backward
+    g = torch.Generator().manual_seed(100 + r)
+    x, y = torch.randn(4, 3, 8, 8, generator=g).to(dev), torch.randint(0, 10, (4,), generator=g).to(dev)
+    for step in range(4):
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(m(x), y)
+        loss.backward()
+        avg = hvd.allreduce(loss.detach().reshape(1), name=f"loss.{step}")   # between bwd and step
+        opt.step()
+        la = hvd.allgather(loss.detach().reshape(1))
+        _close(avg, la.mean().reshape(1), tol=1e-5)
+    torch.cuda.synchronize()
+    for v in seen:
+        _close(v, torch.full((3,), (n + 1) / 2.0, device=dev))
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    allf = hvd.allgather(flat.unsqueeze(0))
+    assert torch.equal(allf[0], allf[-1])
+    hvd.shutdown()
+    print("OK", r)
+
+
+def gpu_rccl_single():
+    """MIVOD_FORCE_COLLECTIVES=1 at world size 1: mivod's own RCCL communicator
+    (csrc/comm) is created and EVERY collective really launches on the GPU —
+    allreduce sum/avg/premul over the dtypes, broadcast, allgather, Adasum, and a
+    DistributedOptimizer step whose bucket allreduce rides RCCL on the comm stream."""
+    from mivod.common import basics as B
+    from mivod.optim import FusedSGD
+    from mivod.parallel import collectives as C
+    hvd.init()
+    st = B.state()
+    assert st.gpu is not None and st.gpu.name == "rccl", st.backend
+    dev = hvd.device()
+    calls0 = C.gpu_stats()["calls"]
+    for dt in (torch.float32, torch.bfloat16, torch.float16, torch.int32, torch.int64):
+        x = (torch.arange(1000, device=dev) % 17).to(dt)
+        y = x.clone()
+        C.allreduce_(y, C.Sum)
+        assert torch.equal(y, x), dt
+        C.allreduce_(y, C.Average)
+        assert torch.equal(y, x), dt
+        if dt.is_floating_point:
+            z = x.clone()
+            C.allreduce_(z, C.Sum, prescale=0.5)
+            torch.testing.assert_close(z.float(), x.float() * 0.5)
+    b = torch.arange(10, device=dev, dtype=torch.float32)
+    C.broadcast_(b, 0)
+    assert torch.equal(b, torch.arange(10, device=dev, dtype=torch.float32))
+    import copy
+    m = _toy(0).to(dev)
+    twin = copy.deepcopy(m)
+    ref = [p.detach().clone() for p in m.parameters()]
+    opt = hvd.DistributedOptimizer(FusedSGD(m.parameters(), lr=0.1),
+                                   named_parameters=m.named_parameters())
+    g = torch.Generator().manual_seed(0)
+    x, yy = torch.randn(4, 3, 8, 8, generator=g).to(dev), torch.randint(0, 10, (4,), generator=g).to(dev)
+    torch.nn.functional.cross_entropy(twin(x), yy).backward()
+    grads = [p.grad.detach().clone() for p in twin.parameters()]   # fused path frees p.grad
+    torch.nn.functional.cross_entropy(m(x), yy).backward()
+    opt.step()
+    torch.cuda.synchronize()
+    for p, q, gr in zip(m.parameters(), ref, grads):
+        torch.testing.assert_close(p.detach(), q - 0.1 * gr, rtol=1e-5, atol=1e-6)
+    calls = C.gpu_stats()["calls"] - calls0
+    assert calls >= 14, calls
+    st.gpu.check()
+    hvd.shutdown()
+    print("OK", 0)
+
 
 def hvd_rank():
     return int(os.environ.get("RANK", "0"))

@@ -118,3 +118,33 @@ def test_schedule_mismatch_raises_on_all_ranks():
     """SURVEY §7.4 risk 4: a differing static bucket schedule raises everywhere."""
     outs = run_ranks("schedule_mismatch", 2)
     assert all(f"raised {r}" in o for r, o in enumerate(outs))
+
+
+# ---- round 2: data-plane features -------------------------------------------
+def test_adasum_vector_halving_4ranks():
+    run_ranks("adasum_vhdd", 4)
+
+
+def test_adasum_vector_halving_2ranks():
+    run_ranks("adasum_vhdd", 2)
+
+
+def test_overflow_guard_skips_step_on_every_rank():
+    run_ranks("overflow_guard", 2)
+
+
+def test_timeline_records_bucket_phases(tmp_path):
+    run_ranks("timeline_buckets", 2, extra_env={"HOROVOD_TIMELINE": str(tmp_path / "tl.json")})
+
+
+def test_prescale_factors_are_not_fused_together():
+    run_ranks("prescale_fusion", 2)
+
+
+@pytest.mark.parametrize("cap", [0, 4, 1024])
+def test_response_cache_capacity(cap):
+    run_ranks("cache_capacity", 2, extra_env={"HOROVOD_CACHE_CAPACITY": str(cap)})
+
+
+def test_checkpoint_resume_keeps_fp32_master_bf16(tmp_path):
+    run_ranks("ckpt_bf16_resume", 2, extra_env={"MIVOD_TEST_DIR": str(tmp_path)})

@@ -16,3 +16,17 @@ def test_gpu_hook_path_two_ranks_one_gpu(cuda):
 def test_gpu_adasum_fp16_two_ranks_one_gpu(cuda):
     """Config-5 path (fp16 wire + Adasum + FusedAdamW) with 2 real ranks on one GPU."""
     run_ranks("gpu_adasum", 2, timeout=180, extra_env={"MIVOD_TRANSPORT": "gloo-gpu"})
+
+
+def test_gpu_named_ops_during_backward_share_one_order(cuda):
+    """hvd.allreduce from a backward hook and between backward and step, on the
+    same communicator/stream as the bucket schedule: no hang, correct averages,
+    bit-identical ranks."""
+    run_ranks("gpu_order", 2, timeout=180, extra_env={"MIVOD_TRANSPORT": "gloo-gpu"})
+
+
+def test_gpu_rccl_communicator_world1(cuda):
+    """mivod's own RCCL communicator (csrc/comm) at world size 1 with the
+    size-1 shortcut disabled: RCCL kernels really run for every collective."""
+    run_ranks("gpu_rccl_single", 1, timeout=180,
+              extra_env={"MIVOD_TRANSPORT": "rccl", "MIVOD_FORCE_COLLECTIVES": "1"})
