@@ -5,6 +5,7 @@
 #include <pybind11/stl.h>
 
 #include "comm.h"
+#include "mesh.h"
 
 namespace py = pybind11;
 using namespace mvcomm;
@@ -93,4 +94,29 @@ PYBIND11_MODULE(_mvcomm, m) {
       .def("destroy", &Comm::destroy, py::call_guard<py::gil_scoped_release>())
       .def("stats", &Comm::stats)
       .def("outstanding", &Comm::outstanding);
+
+  // xGMI mesh one-shot allreduce over HIP-IPC-mapped peer staging buffers
+  py::class_<Mesh>(m, "Mesh")
+      .def(py::init<int, int, int, size_t>(), py::arg("rank"), py::arg("size"),
+           py::arg("device"), py::arg("capacity_bytes"))
+      .def("handles", [](const Mesh& me) { return py::bytes(me.handles()); })
+      .def("open",
+           [](Mesh& me, std::vector<py::bytes> hs) {
+             std::vector<std::string> v;
+             for (auto& h : hs) v.push_back(std::string(h));
+             py::gil_scoped_release nogil;
+             me.open(v);
+           })
+      .def("allreduce",
+           [](Mesh& me, uintptr_t in, uintptr_t out, size_t n, int dt, float scale, uintptr_t s) {
+             me.allreduce((const void*)in, (void*)out, n, dt, scale, s);
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("status", &Mesh::status, py::call_guard<py::gil_scoped_release>())
+      .def("close", &Mesh::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("capacity", &Mesh::capacity)
+      .def_property_readonly("rank", &Mesh::rank)
+      .def_property_readonly("size", &Mesh::size)
+      .def_property_readonly("calls", &Mesh::calls)
+      .def_property_readonly("bytes", &Mesh::bytes);
 }

@@ -161,22 +161,25 @@ def build_comm(verbose: bool = False, force: bool = False) -> str:
     cdir = os.path.join(CSRC, "comm")
     os.makedirs(BUILD, exist_ok=True)
     hdrs = _headers(cdir)
-    srcs = sorted(f for f in os.listdir(cdir) if f.endswith(".cc"))
+    srcs = sorted(f for f in os.listdir(cdir) if f.endswith((".cc", ".hip")))
+    kern_hdrs = _headers(os.path.join(CSRC, "kernels"))
     objs, jobs = [], []
     for f in srcs:
         src = os.path.join(cdir, f)
         obj = os.path.join(BUILD, "comm_" + f + ".o")
         objs.append(obj)
-        if force or _stale(obj, [src] + hdrs):
-            jobs.append([_hipcc(), "-O2", "-std=c++17", "-fPIC", "-Wall", "-fvisibility=hidden",
-                         "-I", cdir, "-I", os.path.join(ROCM, "include")]
+        if force or _stale(obj, [src] + hdrs + kern_hdrs):
+            dev = [f"--offload-arch={ARCH}"] if f.endswith(".hip") else []
+            jobs.append([_hipcc()] + dev + ["-O3", "-std=c++17", "-fPIC", "-Wall",
+                                            "-fvisibility=hidden", "-I", cdir,
+                                            "-I", os.path.join(ROCM, "include")]
                         + [x for p in _py_includes() for x in ("-I", p)]
                         + ["-c", src, "-o", obj])
     _parallel(jobs, verbose)
     so = comm_so()
     tl = _torch_libdir()
     if force or jobs or _stale(so, objs):
-        _run([_hipcc(), "-shared", "-fPIC", "-o", so] + objs
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs
              + ["-L", tl, f"-Wl,-rpath,{tl}", "-l:librccl.so", "-l:libamdhip64.so",
                 "-lpthread"], verbose)
     return so

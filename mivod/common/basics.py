@@ -61,6 +61,7 @@ class _State:
         self.gpu = None          # GPU transport (RcclTransport / PgTransport)
         self.gpu_local = None    # ncclCommSplit intra-node child
         self.gpu_cross = None    # ncclCommSplit cross-node child
+        self.mesh = None         # xGMI mesh one-shot allreduce (small buckets)
         self.comm_stream = None
         self.rings = None        # native CPU data plane: [main ring, engine ring] (tcp_ring.py)
         self.init_count = 0
@@ -168,7 +169,7 @@ def init(comm=None, process_sets=None):
         if transport == "nccl":
             transport = "rccl"
         from ..parallel.order import ORDER
-        _state.gpu = _state.gpu_local = _state.gpu_cross = None
+        _state.gpu = _state.gpu_local = _state.gpu_cross = _state.mesh = None
         _state.init_count += 1
         if _state.size > 1:
             if not dist.is_initialized():
@@ -192,6 +193,7 @@ def init(comm=None, process_sets=None):
             _state.rings = make_rings(_state, generation=_state.init_count)
             if use_gpu:
                 _make_gpu_plane(transport, world_backend, cfg)
+                _make_mesh()
             else:
                 _state.backend = "gloo"
         else:
@@ -255,6 +257,18 @@ def _make_gpu_plane(transport: str, world_backend: str, cfg) -> None:
                 _state.gpu_cross = PgTransport(g, staged=staged, name=_state.gpu.name)
 
 
+def _make_mesh() -> None:
+    """MIVOD_MESH_MAX_MB > 0 and every rank on this node: the xGMI mesh one-shot
+    allreduce serves buckets up to that size (csrc/comm/mesh.hip)."""
+    mb = float(os.environ.get("MIVOD_MESH_MAX_MB", "0") or 0)
+    if mb <= 0 or _state.local_size != _state.size or _state.size > 16:
+        return
+    from ..parallel.transport import MeshTransport
+    store = dist.distributed_c10d._get_default_store()
+    _state.mesh = MeshTransport(_state.rank, _state.size, _state.device, int(mb * 2 ** 20), store,
+                                key=f"mivod/mesh/{_state.init_count}")
+
+
 def _make_hierarchy_groups():
     """Intra-node and cross-node gloo groups (hierarchical CPU allreduce).
     Every rank must create every group, in the same order."""
@@ -294,13 +308,13 @@ def shutdown():
             for r in _state.rings:
                 r.close()
             _state.rings = None
-        for tr in (_state.gpu_local, _state.gpu_cross, _state.gpu):
+        for tr in (_state.mesh, _state.gpu_local, _state.gpu_cross, _state.gpu):
             if tr is not None:
                 try:
                     tr.close()
                 except Exception as e:  # pragma: no cover
                     log.warning("mivod GPU transport shutdown error: %s", e)
-        _state.gpu = _state.gpu_local = _state.gpu_cross = None
+        _state.gpu = _state.gpu_local = _state.gpu_cross = _state.mesh = None
         if _state.owns_pg and dist.is_initialized():
             try:
                 dist.destroy_process_group()

@@ -88,6 +88,9 @@ def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
                 if prescale != 1.0:
                     flat.mul_(prescale)
                 adasum_allreduce_(flat, adasum_table, tr)
+            elif (st.mesh is not None and group is None and op in (Average, Sum)
+                  and st.mesh.accepts(flat, _TOP[op])):
+                st.mesh.allreduce_(flat, _TOP[op], prescale)     # small bucket: one xGMI hop
             elif (st.config is not None and st.config.hierarchical_allreduce and group is None
                   and st.gpu_local is not None and st.gpu_cross is not None):
                 _hierarchical_gpu_(flat, op, prescale)
@@ -314,6 +317,10 @@ def max_over_ranks(x: float) -> float:
 
 
 def gpu_stats() -> dict:
-    """Cumulative calls / bytes of the GPU transport (empty without one)."""
+    """Cumulative calls / bytes of the GPU transport (+ mesh; empty without one)."""
     st = basics.state()
-    return st.gpu.stats() if st.gpu is not None else {}
+    out = dict(st.gpu.stats()) if st.gpu is not None else {}
+    if st.mesh is not None:
+        out.update(st.mesh.stats())
+        out["calls"] = out.get("calls", 0) + out["mesh_calls"]
+    return out

@@ -276,3 +276,44 @@ class PgTransport:
 
     def close(self):
         pass
+
+
+class MeshTransport:
+    """xGMI mesh one-shot allreduce (``mivod._mvcomm.Mesh``, csrc/comm/mesh.hip) for
+    small buckets: every rank reads every peer's HIP-IPC-mapped staging copy and
+    reduces locally in fixed rank order (bit-identical on all ranks).  Used for
+    Sum/Average of fp32/bf16/fp16 buffers of at most ``MIVOD_MESH_MAX_MB``; all
+    ranks must share one node.  Parity: SURVEY.md §2.5 K7."""
+
+    name = "mesh"
+    _CODES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+    def __init__(self, rank: int, size: int, device: torch.device, capacity_bytes: int, store,
+                 key: str):
+        m = _mvcomm()
+        self.rank, self.size = rank, size
+        self.mesh = m.Mesh(rank, size, device.index, int(capacity_bytes))
+        store.set(f"{key}/{rank}", self.mesh.handles())
+        hs = [bytes(store.get(f"{key}/{r}")) for r in range(size)]
+        self.mesh.open(hs)
+        self.capacity = self.mesh.capacity
+
+    def accepts(self, t: torch.Tensor, op: str) -> bool:
+        return (op in (SUM, AVG) and t.dtype in self._CODES and t.is_contiguous()
+                and t.numel() * t.element_size() <= self.capacity
+                and t.data_ptr() % 16 == 0)
+
+    def allreduce_(self, t: torch.Tensor, op: str = SUM, prescale: float = 1.0) -> torch.Tensor:
+        scale = float(prescale) * (1.0 / self.size if op == AVG else 1.0)
+        self.mesh.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), self._CODES[t.dtype], scale,
+                            _stream())
+        return t
+
+    def status(self) -> int:
+        return self.mesh.status()
+
+    def stats(self) -> dict:
+        return {"mesh_calls": self.mesh.calls, "mesh_bytes": self.mesh.bytes}
+
+    def close(self):
+        self.mesh.close()

@@ -966,6 +966,93 @@ def gpu_rccl_single():
     print("OK", 0)
 
 
+def gpu_mesh():
+    """xGMI mesh one-shot allreduce (csrc/comm/mesh.hip) with 2 real ranks on one GPU
+    (HIP IPC between the two processes): bitwise equal to the reference wire
+    (gloo-gpu), deterministic across repeats, identical on both ranks; then a
+    DistributedOptimizer whose small buckets ride the mesh keeps ranks identical."""
+    from mivod.common import basics as B
+    from mivod.optim import FusedSGD
+    from mivod.parallel import collectives as C
+    from mivod.parallel import transport as T
+    hvd.init()
+    r, n = hvd.rank(), hvd.size()
+    dev = hvd.device()
+    st = B.state()
+    assert st.mesh is not None, "mesh not created"
+    for dt in (torch.float32, torch.bfloat16, torch.float16):
+        for cnt in (1, 7, 8, 64, 1000, 65536 + 3, 200000):
+            g = torch.Generator().manual_seed(cnt * 10 + r)
+            x = (torch.randn(cnt, generator=g) * 3).to(dt).to(dev)
+            ref = x.clone()
+            st.gpu.allreduce_(ref, T.SUM)                   # the gloo-gpu wire, no mesh
+            y = x.clone()
+            calls = st.mesh.mesh.calls
+            C.allreduce_(y, C.Sum)
+            assert st.mesh.mesh.calls == calls + 1, "allreduce did not take the mesh"
+            torch.cuda.synchronize()
+            assert torch.equal(y, ref), (dt, cnt, (y.float() - ref.float()).abs().max())
+            y2 = x.clone()
+            C.allreduce_(y2, C.Sum)
+            assert torch.equal(y, y2), "mesh not deterministic"
+            a = x.clone()
+            C.allreduce_(a, C.Average)
+            torch.testing.assert_close(a.float(), ref.float() / n, rtol=1e-2, atol=1e-2)
+            allb = hvd.allgather(y.float().unsqueeze(0))
+            assert torch.equal(allb[0], allb[-1])
+    big = torch.ones(2 * 2 ** 20, device=dev)                   # 8 MB > 1 MB: RCCL/gloo path
+    calls = st.mesh.mesh.calls
+    C.allreduce_(big, C.Sum)
+    assert st.mesh.mesh.calls == calls and float(big[0]) == n
+    torch.manual_seed(0)
+    m = _toy(0).to(dev)
+    opt = hvd.DistributedOptimizer(FusedSGD(m.parameters(), lr=0.05, momentum=0.9),
+                                   named_parameters=m.named_parameters(),
+                                   bucket_mb=0.002, first_bucket_mb=0.001)
+    gg = torch.Generator().manual_seed(100 + r)
+    x, y = torch.randn(4, 3, 8, 8, generator=gg).to(dev), torch.randint(0, 10, (4,), generator=gg).to(dev)
+    calls = st.mesh.mesh.calls
+    for _ in range(3):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    assert st.mesh.mesh.calls >= calls + 3 * len(opt.bucket_plan())
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    allf = hvd.allgather(flat.unsqueeze(0))
+    assert torch.equal(allf[0], allf[-1])
+    assert st.mesh.status() == 0
+    hvd.shutdown()
+    print("OK", r)
+
+
+def gpu_mesh_bench():
+    """Timing of the mesh allreduce (for rocprof): 2 ranks on one GPU, 64 KB - 4 MB."""
+    from mivod.common import basics as B
+    from mivod.parallel import collectives as C
+    hvd.init()
+    r = hvd.rank()
+    dev = hvd.device()
+    assert B.state().mesh is not None
+    for kb in (64, 256, 1024, 4096):
+        x = torch.randn(kb * 256, device=dev).to(torch.bfloat16)     # kb KiB of bf16 x2
+        for _ in range(5):
+            C.allreduce_(x, C.Sum)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(50):
+            C.allreduce_(x, C.Sum)
+        e1.record()
+        torch.cuda.synchronize()
+        if r == 0:
+            print(f"mesh allreduce {kb * 512 // 1024} KiB bf16: {e0.elapsed_time(e1) / 50 * 1000:.1f} us",
+                  flush=True)
+    assert B.state().mesh.status() == 0
+    hvd.shutdown()
+    print("OK", r)
+
+
 def hvd_rank():
     return int(os.environ.get("RANK", "0"))
 

@@ -30,3 +30,9 @@ def test_gpu_rccl_communicator_world1(cuda):
     size-1 shortcut disabled: RCCL kernels really run for every collective."""
     run_ranks("gpu_rccl_single", 1, timeout=180,
               extra_env={"MIVOD_TRANSPORT": "rccl", "MIVOD_FORCE_COLLECTIVES": "1"})
+
+
+def test_gpu_xgmi_mesh_one_shot_allreduce(cuda):
+    """K7: the HIP-IPC mesh allreduce kernel between two processes on one GPU."""
+    run_ranks("gpu_mesh", 2, timeout=180,
+              extra_env={"MIVOD_TRANSPORT": "gloo-gpu", "MIVOD_MESH_MAX_MB": "1"})
