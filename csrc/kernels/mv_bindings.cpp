@@ -13,6 +13,7 @@
 #include "mv_attn.h"
 #include "mv_bert.h"
 #include "mv_bn.h"
+#include "mv_gemm.h"
 #include "mv_kernels.h"
 #include "mv_pool.h"
 
@@ -311,7 +312,8 @@ std::vector<at::Tensor> bn_fwd_train_impl(at::Tensor x, c10::optional<at::Tensor
                                           c10::optional<at::Tensor> running_mean,
                                           c10::optional<at::Tensor> running_var, double momentum,
                                           double eps, bool relu,
-                                          c10::optional<at::Tensor> residual, bool want_mask) {
+                                          c10::optional<at::Tensor> residual, bool want_mask,
+                                          c10::optional<at::Tensor> stats = c10::nullopt) {
   int64_t C;
   const int64_t M = bn_check_act(x, "x", &C);
   TORCH_CHECK(M > 0, "bn: empty input");
@@ -326,7 +328,7 @@ std::vector<at::Tensor> bn_fwd_train_impl(at::Tensor x, c10::optional<at::Tensor
   }
   auto fo = x.options().dtype(at::kFloat);
   const int P = mv_bn_partials(M, (int)C);
-  at::Tensor partial = at::empty({(int64_t)P * 2 * C}, fo);
+  at::Tensor partial = stats.has_value() ? at::Tensor() : at::empty({(int64_t)P * 2 * C}, fo);
   at::Tensor vec = at::empty({4, C}, fo);   // save_mean, save_invstd, scale, bias
   at::Tensor y = at::empty_like(x);
   at::Tensor mask;
@@ -337,11 +339,26 @@ std::vector<at::Tensor> bn_fwd_train_impl(at::Tensor x, c10::optional<at::Tensor
   float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
   float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
   TORCH_CHECK((rm == nullptr) == (rv == nullptr), "bn: running_mean/var must both be given");
-  mv_bn_fwd_train(x.data_ptr(), rp, y.data_ptr(), M, (int)C, rm, rv, opt_f32(gamma, C, "weight"),
-                  opt_f32(beta, C, "bias"), (float)momentum, (float)eps, relu,
-                  partial.data_ptr<float>(), P, vec[0].data_ptr<float>(),
-                  vec[1].data_ptr<float>(), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
-                  cur_stream(), want_mask ? mask.data_ptr() : nullptr);
+  if (stats.has_value()) {
+    // statistics from the producing conv's epilogue: [P, 2, C] partials around rm
+    TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kFloat && stats->is_contiguous() &&
+                    stats->dim() == 3 && stats->size(1) == 2 && stats->size(2) == C &&
+                    stats->size(0) > 0,
+                "bn: stats must be fp32 [P, 2, C] partials");
+    mv_bn_fwd_from_partials(x.data_ptr(), rp, y.data_ptr(), M, (int)C, rm, rv,
+                            opt_f32(gamma, C, "weight"), opt_f32(beta, C, "bias"),
+                            (float)momentum, (float)eps, relu, stats->data_ptr<float>(),
+                            (int)stats->size(0), vec[0].data_ptr<float>(),
+                            vec[1].data_ptr<float>(), vec[2].data_ptr<float>(),
+                            vec[3].data_ptr<float>(), cur_stream(),
+                            want_mask ? mask.data_ptr() : nullptr);
+  } else {
+    mv_bn_fwd_train(x.data_ptr(), rp, y.data_ptr(), M, (int)C, rm, rv, opt_f32(gamma, C, "weight"),
+                    opt_f32(beta, C, "bias"), (float)momentum, (float)eps, relu,
+                    partial.data_ptr<float>(), P, vec[0].data_ptr<float>(),
+                    vec[1].data_ptr<float>(), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
+                    cur_stream(), want_mask ? mask.data_ptr() : nullptr);
+  }
   if (want_mask) return {y, vec, mask};
   return {y, vec};
 }
@@ -353,6 +370,18 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> gam
                                      double eps, bool relu, c10::optional<at::Tensor> residual) {
   return bn_fwd_train_impl(x, gamma, beta, running_mean, running_var, momentum, eps, relu,
                            residual, false);
+}
+
+// forward with statistics partials from the conv GEMM epilogue ({y, vec} or {y, vec, mask})
+std::vector<at::Tensor> bn_fwd_train_stats(at::Tensor x, at::Tensor stats,
+                                           c10::optional<at::Tensor> gamma,
+                                           c10::optional<at::Tensor> beta,
+                                           c10::optional<at::Tensor> running_mean,
+                                           c10::optional<at::Tensor> running_var, double momentum,
+                                           double eps, bool relu,
+                                           c10::optional<at::Tensor> residual, bool want_mask) {
+  return bn_fwd_train_impl(x, gamma, beta, running_mean, running_var, momentum, eps, relu,
+                           residual, want_mask, stats);
 }
 
 // {y, vec, mask}: add+ReLU forward that also records the backward bitmask (mode 3)
@@ -761,6 +790,43 @@ at::Tensor pad_channels(at::Tensor x, int64_t cout) {
   return y;
 }
 
+// ---------------------------------------------------------------------------
+// NT GEMM for NHWC 1x1 convolutions (+ fused BN statistics epilogue)
+// ---------------------------------------------------------------------------
+int64_t gemm_partials(int64_t M, int64_t N, int64_t K) {
+  return mv_gemm_partials(M, (int)N, (int)K);
+}
+
+void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> shift,
+             c10::optional<at::Tensor> partial) {
+  for (const at::Tensor* t : {&a, &b, &c})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
+                    t->dim() == 2,
+                "gemm_nt: A, B, C must be contiguous 2-D bf16 GPU tensors");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_nt: shape mismatch");
+  TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && K > 0 && N > 0 && M > 0,
+              "gemm_nt: K and N must be positive multiples of 64");
+  TORCH_CHECK(a.device() == b.device() && a.device() == c.device(), "gemm_nt: devices differ");
+  TORCH_CHECK(M * K < (int64_t(1) << 40) && M * N < (int64_t(1) << 40), "gemm_nt: too large");
+  TORCH_CHECK((M + 63) / 64 * (N / 64) < (int64_t(1) << 31), "gemm_nt: grid too large");
+  float* pp = nullptr;
+  const float* sp = nullptr;
+  if (partial.has_value()) {
+    TORCH_CHECK(partial->is_cuda() && partial->scalar_type() == at::kFloat &&
+                    partial->is_contiguous() && partial->numel() >= gemm_partials(M, N, K) * 2 * N,
+                "gemm_nt: partial must be fp32 [P, 2, N] with P = gemm_partials(M, N)");
+    pp = partial->data_ptr<float>();
+    if (shift.has_value()) {
+      TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->numel() == N,
+                  "gemm_nt: shift must be fp32 [N]");
+      sp = shift->data_ptr<float>();
+    }
+  }
+  c10::DeviceGuard guard(a.device());
+  mv_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, (int)N, (int)K, sp, pp, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -793,6 +859,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("bn_fwd_train_mask", &bn_fwd_train_mask,
         "fused NHWC BN+add+ReLU training forward that also returns the backward bitmask");
   m.def("bn_apply", &bn_apply, "NHWC y = act(x*scale + bias (+res))");
+  m.def("bn_fwd_train_stats", &bn_fwd_train_stats,
+        "fused BN(+add)(+ReLU) forward from the conv epilogue's statistics partials");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward (+ second grad stream)");
   m.def("bn_stats", &bn_stats, "NHWC BN training statistics only -> [4, C]");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC maxpool with fused affine+ReLU prologue -> (y, idx)");
@@ -800,4 +868,6 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gap_fwd", &gap_fwd, "NHWC global average pool -> [N, C]");
   m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
   m.def("pad_channels", &pad_channels, "NHWC zero channel padding C -> cout (<= 8)");
+  m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics");
+  m.def("gemm_partials", &gemm_partials, "row tiles (statistics partial rows) of gemm_nt");
 }

@@ -12,6 +12,13 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
                      bool relu, float* partial, int P, float* save_mean, float* save_invstd,
                      float* scale, float* bias, hipStream_t st, void* mask = nullptr);
 
+// finalize + apply from [P][2][C] statistics partials produced by the conv GEMM epilogue
+void mv_bn_fwd_from_partials(const void* x, const void* res, void* y, int64_t M, int C,
+                             float* rmean, float* rvar, const float* gamma, const float* beta,
+                             float momentum, float eps, bool relu, const float* partial, int P,
+                             float* save_mean, float* save_invstd, float* scale, float* bias,
+                             hipStream_t st, void* mask = nullptr);
+
 void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
                  const float* bias, bool relu, hipStream_t st, void* mask = nullptr);
 // mask (add+ReLU only, may be null): [M, C/8] bytes, bit j of byte (r, c/8) = y[r, c+j] > 0

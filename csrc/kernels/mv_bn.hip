@@ -614,6 +614,20 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
   if (y) mv_bn_apply(x, res, y, M, C, scale, bias, relu, st, mask);   // y == null: statistics only
 }
 
+// The statistics were produced elsewhere (the 1x1 conv GEMM's fused epilogue,
+// mv_gemm.hip): [P][2][C] partials around shift = running mean, same layout as
+// stats_kernel's.  Finalize (+ running-stat update) and apply only.
+void mv_bn_fwd_from_partials(const void* x, const void* res, void* y, int64_t M, int C,
+                             float* rmean, float* rvar, const float* gamma, const float* beta,
+                             float momentum, float eps, bool relu, const float* partial, int P,
+                             float* save_mean, float* save_invstd, float* scale, float* bias,
+                             hipStream_t st, void* mask) {
+  hipLaunchKernelGGL(finalize_fwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
+                     partial, P, M, C, rmean, rvar, gamma, beta, momentum, eps, save_mean,
+                     save_invstd, scale, bias);
+  if (y) mv_bn_apply(x, res, y, M, C, scale, bias, relu, st, mask);
+}
+
 // apply / dx passes: 2 rows in flight per lane; MIVOD_BN_APPLY_U=4 selects 4 (measured
 // equal on the bs512 shapes, scripts/micro_bn.py)
 static bool apply_u2() {

@@ -1,0 +1,451 @@
+// NT GEMM on gfx950 MFMA for NHWC 1x1 convolutions, with fused epilogues.
+//
+//   C[M, N] (bf16) = A[M, K] (bf16, row-major: NHWC activations) . B[N, K]^T (bf16,
+//   row-major: a channels_last [Cout, Cin, 1, 1] filter; for the data gradient the
+//   channel-transposed filter)                              fp32 accumulation
+//
+// Epilogue STATS (the following BatchNorm's statistics pass, fused): per output
+// channel n, over this workgroup's rows, s1 = sum(c - shift[n]), s2 = sum((c -
+// shift[n])^2) of the bf16-ROUNDED outputs, written as partial[blockM][2][N] in a
+// fixed order — the exact layout the BN finalize kernel (mv_bn.hip) reduces, so
+// the statistics are deterministic and bit-identical on every rank, and the
+// separate full read of C by the statistics pass disappears.
+//
+// MFMA mapping (v_mfma_f32_16x16x32_bf16): the FILTER tile is the A operand and the
+// activation tile the B operand, so D = W . A^T = C^T and each lane's 4 accumulator
+// registers are 4 CONSECUTIVE output channels of one output row — an 8-byte store
+// per 16x16 tile, and the per-channel statistics reduce across the 16 lanes of a
+// lane group with 4 xor-shuffles.
+//
+// Staging: global -> registers (16-byte loads) -> LDS double buffer with a 16-byte
+// chunk XOR swizzle (row r's chunk c lives at c ^ (r & 7)), one barrier per
+// 64-deep K step.  Grid: 1-D, tiles remapped so the N tiles of one row block are
+// consecutive on one XCD (they share the activation rows through that XCD's L2).
+#include "mv_common.h"
+#include "mv_gemm.h"
+
+#include <cstdlib>
+
+namespace mv {
+namespace gemm {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int BK = 64;
+constexpr int KC = BK / 8;          // 16-byte chunks per staged row
+
+__device__ __forceinline__ f32x4v mfma(const bf16x8& a, const bf16x8& b, const f32x4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ (row & 7)) << 3); }
+
+__device__ __forceinline__ float round_bf16(float x) { return (float)(__bf16)x; }
+
+// bijective XCD-aware remap of the 1-D workgroup id (8 XCDs, round-robin dispatch)
+__device__ __forceinline__ int remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+template <int BM, int BN, int WM, int WN, bool STATS>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
+    int64_t M, int N, int K, int ntn, const float* __restrict__ shift,
+    float* __restrict__ partial) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int A_CH = BM * KC / NT;
+  constexpr int B_CH = BN * KC / NT;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int STAGE = (BM + BN) * BK;
+  static_assert(BM * KC % NT == 0 && BN * KC % NT == 0, "tile / thread mismatch");
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int t = remap(blockIdx.x, gridDim.x);
+  const int mt = t / ntn, nt = t - mt * ntn;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+
+  u32x4 ra[A_CH], rb[B_CH];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int q = tid + i * NT, row = q / KC, ch = q % KC;
+      int64_t gm = m0 + row;
+      gm = gm < M ? gm : M - 1;                 // rows past M: read a valid row, never stored
+      ra[i] = *reinterpret_cast<const u32x4*>(A + gm * K + k0 + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int q = tid + i * NT, row = q / KC, ch = q % KC;
+      rb[i] = *reinterpret_cast<const u32x4*>(B + (int64_t)(n0 + row) * K + k0 + ch * 8);
+    }
+  };
+  auto sstore = [&](int buf) {
+    __bf16* As = smem + buf * STAGE;
+    __bf16* Bs = As + BM * BK;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int q = tid + i * NT, row = q / KC, ch = q % KC;
+      *reinterpret_cast<u32x4*>(As + swz(row, ch)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int q = tid + i * NT, row = q / KC, ch = q % KC;
+      *reinterpret_cast<u32x4*>(Bs + swz(row, ch)) = rb[i];
+    }
+  };
+
+  f32x4v acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = K / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + 1 < KT) gload((kt + 1) * BK);
+    const __bf16* As = smem + (kt & 1) * STAGE;
+    const __bf16* Bs = As + BM * BK;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int ch = kk * 4 + (lane >> 4);
+      bf16x8 wf[TN], af[TM];
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+        wf[a] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WTN + a * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int b = 0; b < TM; ++b)
+        af[b] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WTM + b * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = mfma(wf[a], af[b], acc[a][b]);
+    }
+    if (kt + 1 < KT) sstore((kt + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[row][col .. col+3] for every (a, b) tile ----
+  const int g = lane >> 4, rl = lane & 15;
+  float s1[TN][4], s2[TN][4];
+#pragma unroll
+  for (int a = 0; a < TN; ++a) {
+    const int col = n0 + wn * WTN + a * 16 + 4 * g;
+    float sh[4] = {0.f, 0.f, 0.f, 0.f};
+    if (STATS && shift) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sh[r] = shift[col + r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[a][r] = 0.f; s2[a][r] = 0.f; }
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int64_t row = m0 + wm * WTM + b * 16 + rl;
+      if (row < M) {
+        const f32x4v v = acc[a][b];
+        u32x2 o = {cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3])};
+        *reinterpret_cast<u32x2*>(C + row * N + col) = o;
+        if (STATS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = round_bf16(v[r]) - sh[r];
+            s1[a][r] += d;
+            s2[a][r] += d * d;
+          }
+        }
+      }
+    }
+  }
+  if (!STATS) return;
+  // reduce over the 16 lanes (rows) of each lane group: fixed xor tree
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[a][r] += __shfl_xor(s1[a][r], o, kWave);
+        s2[a][r] += __shfl_xor(s2[a][r], o, kWave);
+      }
+    }
+  // combine the WM waves of a column in a fixed order through LDS (reuses the stage)
+  float* red = reinterpret_cast<float*>(smem);      // [2][WM][BN]
+  if (rl == 0) {
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = wn * WTN + a * 16 + 4 * g + r;
+        red[(0 * WM + wm) * BN + c] = s1[a][r];
+        red[(1 * WM + wm) * BN + c] = s2[a][r];
+      }
+  }
+  __syncthreads();
+  for (int v = tid; v < 2 * BN; v += NT) {
+    const int k = v / BN, c = v - k * BN;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) s += red[(k * WM + w) * BN + c];
+    partial[((int64_t)mt * 2 + k) * N + n0 + c] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight-stationary streaming variant for small K (64 / 128 / 256): the skinny,
+// HBM-bound 1x1 convs of ResNet's early stages.  A persistent workgroup keeps its
+// [BN, K] filter slice in LDS for the whole kernel and streams 64-row tiles of A:
+// the next tile's 16-byte global loads are in flight (in registers) while the
+// current tile is multiplied and stored, and the fused statistics accumulate in
+// registers across ALL the tiles a workgroup processes — one cross-lane reduction
+// and one [2][BN] partial row per workgroup at the very end.  The 4 waves split
+// the BN columns (64 each), 64 rows x 64 columns per wave per tile.
+// ---------------------------------------------------------------------------
+template <int K, int BN, bool STATS>
+__global__ __launch_bounds__(256) void gemm_stream_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
+    int64_t M, int N, int ntn, int64_t ntm, const float* __restrict__ shift,
+    float* __restrict__ partial) {
+  constexpr int BM = 64;
+  constexpr int KCH = K / 8;                 // 16-byte chunks per row
+  constexpr int A_CH = BM * KCH / 256;       // A chunks per thread per tile
+  constexpr int W_CH = BN * KCH / 256;
+  constexpr int WTN = BN / 4;                // columns per wave
+  constexpr int TN = WTN / 16, TM = BM / 16;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[(BN + BM) * K];
+  __bf16* Ws = smem;
+  __bf16* As = smem + BN * K;
+  auto sw = [](int row, int ch) { return row * K + ((ch ^ (row & 7)) << 3); };
+
+  const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
+  const int g = lane >> 4, rl = lane & 15;
+  const int t = remap(blockIdx.x, gridDim.x);
+  const int nt = t % ntn;
+  const int64_t stream = t / ntn, nstreams = gridDim.x / ntn;
+  const int n0 = nt * BN;
+
+  // filter slice -> LDS (once)
+#pragma unroll
+  for (int i = 0; i < W_CH; ++i) {
+    const int q = tid + i * 256, row = q / KCH, ch = q % KCH;
+    *reinterpret_cast<u32x4*>(Ws + sw(row, ch)) =
+        *reinterpret_cast<const u32x4*>(B + (int64_t)(n0 + row) * K + ch * 8);
+  }
+  u32x4 ra[A_CH];
+  auto gload = [&](int64_t mt) {
+    const int64_t m0 = mt * BM;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int q = tid + i * 256, row = q / KCH, ch = q % KCH;
+      int64_t gm = m0 + row;
+      gm = gm < M ? gm : M - 1;
+      ra[i] = *reinterpret_cast<const u32x4*>(A + gm * K + ch * 8);
+    }
+  };
+  float sh[TN][4], s1[TN][4], s2[TN][4];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sh[a][r] = (STATS && shift) ? shift[n0 + wn * WTN + a * 16 + 4 * g + r] : 0.f;
+      s1[a][r] = 0.f;
+      s2[a][r] = 0.f;
+    }
+  int64_t mt = stream;
+  if (mt < ntm) gload(mt);
+  for (; mt < ntm; mt += nstreams) {
+    __syncthreads();                                   // previous tile's LDS reads done
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int q = tid + i * 256, row = q / KCH, ch = q % KCH;
+      *reinterpret_cast<u32x4*>(As + sw(row, ch)) = ra[i];
+    }
+    __syncthreads();
+    if (mt + nstreams < ntm) gload(mt + nstreams);     // in flight during compute + stores
+    f32x4v acc[TN][TM];
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+      for (int b = 0; b < TM; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < K / 32; ++kk) {
+      const int ch = kk * 4 + g;
+      bf16x8 wf[TN], af[TM];
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+        wf[a] = *reinterpret_cast<const bf16x8*>(Ws + sw(wn * WTN + a * 16 + rl, ch));
+#pragma unroll
+      for (int b = 0; b < TM; ++b)
+        af[b] = *reinterpret_cast<const bf16x8*>(As + sw(b * 16 + rl, ch));
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = mfma(wf[a], af[b], acc[a][b]);
+    }
+    const int64_t m0 = mt * BM;
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int64_t row = m0 + b * 16 + rl;
+      if (row < M) {
+#pragma unroll
+        for (int a = 0; a < TN; ++a) {
+          const f32x4v v = acc[a][b];
+          const uint32_t p0 = cvt_pk_bf16(v[0], v[1]), p1 = cvt_pk_bf16(v[2], v[3]);
+          u32x2 o = {p0, p1};
+          *reinterpret_cast<u32x2*>(C + row * N + n0 + wn * WTN + a * 16 + 4 * g) = o;
+          if (STATS) {
+            const float q[4] = {__uint_as_float(p0 << 16), __uint_as_float(p0 & 0xffff0000u),
+                                __uint_as_float(p1 << 16), __uint_as_float(p1 & 0xffff0000u)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float d = q[r] - sh[a][r];
+              s1[a][r] += d;
+              s2[a][r] += d * d;
+            }
+          }
+        }
+      }
+    }
+  }
+  if (!STATS) return;
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[a][r] += __shfl_xor(s1[a][r], o, kWave);
+        s2[a][r] += __shfl_xor(s2[a][r], o, kWave);
+      }
+    }
+  if (rl == 0 && stream < ntm) {
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = n0 + wn * WTN + a * 16 + 4 * g + r;
+        partial[(stream * 2 + 0) * N + c] = s1[a][r];
+        partial[(stream * 2 + 1) * N + c] = s2[a][r];
+      }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+static void launch(const __bf16* A, const __bf16* B, __bf16* C, int64_t M, int N, int K,
+                   const float* shift, float* partial, hipStream_t st) {
+  const int ntn = N / BN;
+  const int64_t ntm = (M + BM - 1) / BM;
+  const dim3 grid((unsigned)(ntm * ntn));
+  if (partial)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, true>), grid, dim3(WM * WN * 64), 0, st, A,
+                       B, C, M, N, K, ntn, shift, partial);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false>), grid, dim3(WM * WN * 64), 0, st,
+                       A, B, C, M, N, K, ntn, shift, partial);
+}
+
+}  // namespace gemm
+}  // namespace mv
+
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+// streaming variant: the BN it uses for (K, N), or false for the tiled kernel
+static bool stream_cfg(int K, int N, int* bn) {
+  const char* e = std::getenv("MIVOD_GEMM_STREAM");
+  if (e && e[0] == '0') return false;
+  if (K == 64 || K == 128) { *bn = N % 256 == 0 ? 256 : (N % 128 == 0 ? 128 : 64); return true; }
+  if (K == 256) { *bn = N % 128 == 0 ? 128 : 64; return true; }
+  return false;
+}
+
+template <int K, int BN, bool STATS>
+static int64_t streams_for(int64_t M, int N) {
+  static int per = [] {
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &v, (const void*)&mv::gemm::gemm_stream_kernel<K, BN, STATS>, 256, 0) != hipSuccess ||
+        v < 1)
+      v = 1;
+    return v;
+  }();
+  const int ntn = N / BN;
+  const int64_t ntm = (M + 63) / 64;
+  int64_t streams = (int64_t)num_cus() * per / ntn;
+  if (streams < 1) streams = 1;
+  if (streams > ntm) streams = ntm;
+  return streams;
+}
+
+template <int K, int BN>
+static void launch_stream(const __bf16* a, const __bf16* b, __bf16* c, int64_t M, int N,
+                          const float* shift, float* partial, hipStream_t st) {
+  using namespace mv::gemm;
+  const int ntn = N / BN;
+  const int64_t ntm = (M + 63) / 64;
+  if (partial) {
+    const dim3 grid((unsigned)(streams_for<K, BN, true>(M, N) * ntn));
+    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, true>), grid, dim3(256), 0, st, a, b, c, M, N,
+                       ntn, ntm, shift, partial);
+  } else {
+    const dim3 grid((unsigned)(streams_for<K, BN, false>(M, N) * ntn));
+    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, false>), grid, dim3(256), 0, st, a, b, c, M, N,
+                       ntn, ntm, shift, partial);
+  }
+}
+
+#define MV_STREAM_CASES(X) \
+  X(64, 256) X(64, 128) X(64, 64) X(128, 256) X(128, 128) X(128, 64) X(256, 128) X(256, 64)
+
+// number of [2][N] statistics partial rows gemm_nt writes for this problem
+int64_t mv_gemm_partials(int64_t M, int N, int K) {
+  int bn;
+  if (stream_cfg(K, N, &bn)) {
+#define MV_P(KK, BB) \
+    if (K == KK && bn == BB) return streams_for<KK, BB, true>(M, N);
+    MV_STREAM_CASES(MV_P)
+#undef MV_P
+  }
+  const int bm = N % 128 == 0 ? 128 : 256;
+  return (M + bm - 1) / bm;
+}
+
+void mv_gemm_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
+                const float* shift, float* partial, hipStream_t st) {
+  using namespace mv::gemm;
+  const __bf16* a = (const __bf16*)A;
+  const __bf16* b = (const __bf16*)B;
+  __bf16* c = (__bf16*)C;
+  int bn;
+  if (stream_cfg(K, N, &bn)) {
+#define MV_L(KK, BB) \
+    if (K == KK && bn == BB) { launch_stream<KK, BB>(a, b, c, M, N, shift, partial, st); return; }
+    MV_STREAM_CASES(MV_L)
+#undef MV_L
+  }
+  if (N % 256 == 0)
+    launch<128, 256, 2, 2>(a, b, c, M, N, K, shift, partial, st);
+  else if (N % 128 == 0)
+    launch<128, 128, 2, 2>(a, b, c, M, N, K, shift, partial, st);
+  else
+    launch<256, 64, 4, 1>(a, b, c, M, N, K, shift, partial, st);
+}

@@ -17,7 +17,7 @@ import os
 import torch.nn.functional as F
 
 from ..ops.conv import Conv2d
-from ..ops.bn import (BatchNorm2d, bn_relu_maxpool, downsample_tap, global_avg_pool,
+from ..ops.bn import (BatchNorm2d, bn_relu_maxpool, conv_bn, downsample_tap, global_avg_pool,
                       pad_channels, tap)
 
 
@@ -70,11 +70,16 @@ class Bottleneck(nn.Module):
             identity = tap(x)
         else:
             conv, rest = self.downsample[0], self.downsample[1:]
-            identity = rest(downsample_tap(x, conv))
-        out = self.bn1(self.conv1(x), relu=True)
+            if conv.stride[0] == 1 and len(rest) == 1 and isinstance(rest[0], BatchNorm2d):
+                identity = conv_bn(conv, rest[0], tap(x))
+            else:
+                identity = rest(downsample_tap(x, conv))
+        # conv_bn: a qualifying 1x1 conv computes its BN's statistics in the GEMM
+        # epilogue (mivod.ops.conv.conv1x1_stats), so the BN skips its statistics pass
+        out = conv_bn(self.conv1, self.bn1, x, relu=True)
         out = self.bn2(self.conv2(out), relu=True)
         # fused: relu(bn3(conv3(out)) + identity) in one pass (mivod.ops.bn)
-        return self.bn3(self.conv3(out), residual=identity, relu=True)
+        return conv_bn(self.conv3, self.bn3, out, relu=True, residual=identity)
 
 
 class ResNet(nn.Module):

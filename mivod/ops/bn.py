@@ -146,10 +146,21 @@ def tap(x: torch.Tensor) -> torch.Tensor:
 class _BNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual,
-                slot):
+                slot, stats=None):
         nat = K.native()
         mode = 2 if (relu and residual is not None) else (1 if relu else 0)
-        if mode == 2 and _BN_MASK:
+        if stats is not None:
+            # statistics came from the producing 1x1 conv's GEMM epilogue (ops.conv)
+            if mode == 2 and _BN_MASK:
+                y, vec, keep = nat.bn_fwd_train_stats(x, stats, weight, bias, running_mean,
+                                                      running_var, momentum, eps, True, residual,
+                                                      True)
+                mode = 3
+            else:
+                y, vec = nat.bn_fwd_train_stats(x, stats, weight, bias, running_mean,
+                                                running_var, momentum, eps, relu, residual, False)
+                keep = y if mode == 2 else None
+        elif mode == 2 and _BN_MASK:
             # add+ReLU: backward reads a 1-bit-per-channel mask of y > 0 (mode 3), not y
             y, vec, keep = nat.bn_fwd_train_mask(x, weight, bias, running_mean, running_var,
                                                  momentum, eps, residual)
@@ -181,12 +192,14 @@ class _BNActTrain(torch.autograd.Function):
         return (dx if ctx.needs_input_grad[0] else None,
                 dg if ctx.needs_input_grad[1] else None,
                 db if ctx.needs_input_grad[2] else None,
-                None, None, None, None, None, dres, None)
+                None, None, None, None, None, dres, None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentum, eps,
-                   relu=False, residual=None):
-    """Functional form: ``act(batch_norm(x) + residual)``."""
+                   relu=False, residual=None, stats=None):
+    """Functional form: ``act(batch_norm(x) + residual)``.  ``stats``: [P, 2, C]
+    statistics partials of x around ``running_mean`` from the producing conv's
+    GEMM epilogue (training only; skips the statistics pass)."""
     if _fusable(x, weight) and (residual is None or (residual.dtype == torch.bfloat16 and
                                                      residual.shape == x.shape)):
         if residual is not None:
@@ -194,7 +207,7 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentu
         if training:
             slot = GradSlot() if (relu and residual is not None) else None
             y = _BNActTrain.apply(x, weight, bias, running_mean, running_var, float(momentum),
-                                  float(eps), bool(relu), residual, slot)
+                                  float(eps), bool(relu), residual, slot, stats)
             if slot is not None:
                 y._mv_slot = slot
             return y
@@ -220,7 +233,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         super().__init__(*a, **kw)
         self._mv_steps = 0   # host-side num_batches_tracked (saves a GPU add per call)
 
-    def forward(self, x, residual=None, relu=False):
+    def forward(self, x, residual=None, relu=False, stats=None):
         self._check_input_dim(x)
         momentum = 0.0 if self.momentum is None else self.momentum
         if self.training and self.track_running_stats:
@@ -230,8 +243,10 @@ class BatchNorm2d(nn.BatchNorm2d):
         bn_training = self.training or (self.running_mean is None and self.running_var is None)
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
+        if stats is not None and not (self.training and self.track_running_stats):
+            stats = None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, bn_training, momentum, self.eps,
-                              relu, residual)
+                              relu, residual, stats)
 
     def _save_to_state_dict(self, destination, prefix, keep_vars):
         if self._mv_steps and self.num_batches_tracked is not None:
@@ -344,3 +359,16 @@ def pad_channels(x: torch.Tensor, cout: int) -> torch.Tensor:
     return F.pad(x, (0, 0, 0, 0, 0, cout - x.shape[1])).contiguous(
         memory_format=torch.channels_last if x.is_contiguous(memory_format=torch.channels_last)
         else torch.contiguous_format)
+
+
+def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = False,
+            residual=None) -> torch.Tensor:
+    """``bn(conv(x), residual, relu)`` with the BN statistics computed inside the
+    1x1 conv's GEMM epilogue when the conv qualifies (ops.conv.stats_fusable) and
+    the BN is training with running statistics; the plain composition otherwise."""
+    from .conv import conv1x1_stats, stats_fusable
+    if (bn.training and bn.track_running_stats and bn.running_mean is not None
+            and _fusable(x, bn.weight) and stats_fusable(conv, x)):
+        y, part = conv1x1_stats(conv, x, bn.running_mean)
+        return bn(y, residual=residual, relu=relu, stats=part)
+    return bn(conv(x), residual=residual, relu=relu)

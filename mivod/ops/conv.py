@@ -17,6 +17,14 @@ The weight gradient still comes from MIOpen's backward-weights solver
 Only stride-1, dilation-1, ungrouped convs with padding ``k // 2`` on channels_last
 bf16 GPU tensors take this path; everything else is a plain ``nn.Conv2d``.
 ``MIVOD_CONV_DGRAD_FWD=0`` disables it (A/B switch).
+
+``conv1x1_stats`` is the forward of a stride-1 1x1 conv as mivod's own MFMA GEMM
+(csrc/kernels/mv_gemm.hip, weight-stationary streaming kernel for K <= 256) with
+the FOLLOWING BatchNorm's statistics computed in the GEMM epilogue — the BN's
+separate statistics pass over the conv output disappears.  Used only where the
+GEMM is at least as fast as MIOpen's kernel (scripts/micro_gemm1x1.py,
+profiles/r2_gemm1x1_fused_stats.md); its backward is the same forward-conv dgrad
++ MIOpen wgrad as above.
 """
 from __future__ import annotations
 
@@ -63,6 +71,55 @@ def _eligible(m: nn.Conv2d, x: torch.Tensor) -> bool:
             and tuple(m.dilation) == (1, 1) and k[0] == k[1] and k[0] % 2 == 1
             and tuple(m.padding) == (k[0] // 2, k[1] // 2) and m.padding_mode == "zeros"
             and x.is_contiguous(memory_format=torch.channels_last))
+
+
+class _Conv1x1Stats(torch.autograd.Function):
+    """y = conv1x1(x, w) via mv_gemm (NHWC GEMM) + [P, 2, Cout] BN statistics
+    partials of y around ``shift`` (non-differentiable side output)."""
+
+    @staticmethod
+    def forward(ctx, x, w, shift):
+        from . import kernels as K
+        nat = K.native()
+        n, cin, h, wd = x.shape
+        cout = w.shape[0]
+        m = n * h * wd
+        a = x.permute(0, 2, 3, 1).reshape(m, cin)            # NHWC view, no copy
+        b = w.permute(0, 2, 3, 1).reshape(cout, cin)
+        yf = torch.empty(m, cout, dtype=x.dtype, device=x.device)
+        part = torch.empty(nat.gemm_partials(m, cout, cin), 2, cout, dtype=torch.float32,
+                           device=x.device)
+        nat.gemm_nt(a, b, yf, shift, part)
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(part)
+        return yf.view(n, h, wd, cout).permute(0, 3, 1, 2), part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = F.conv2d(dy, _transposed_filter(w))
+        if ctx.needs_input_grad[1]:
+            _, dw, _ = torch.ops.aten.convolution_backward(
+                dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])
+        return dx, dw, None
+
+
+def stats_fusable(m: nn.Conv2d, x: torch.Tensor) -> bool:
+    """1x1 / stride 1 convs whose forward mivod's GEMM runs at least as fast as
+    MIOpen (K = Cin in {64, 128, 256}, or Cin 512 -> Cout 128 on MI355X)."""
+    if os.environ.get("MIVOD_CONV_BN_FUSE", "1") == "0" or not _eligible(m, x):
+        return False
+    cin, cout = m.in_channels, m.out_channels
+    return (tuple(m.kernel_size) == (1, 1) and cout % 64 == 0
+            and (cin in (64, 128, 256) or (cin == 512 and cout == 128)))
+
+
+def conv1x1_stats(m: nn.Conv2d, x: torch.Tensor, shift):
+    """(y, partial) — see _Conv1x1Stats; ``shift`` is the BN's running mean."""
+    return _Conv1x1Stats.apply(x, m.weight, shift)
 
 
 class Conv2d(nn.Conv2d):

@@ -1,0 +1,79 @@
+"""Microbenchmark: ResNet-50 bs2048 1x1 conv forwards — MIOpen/CK (F.conv2d) vs
+mivod's MFMA NT GEMM (mv_gemm.hip), plain and with the fused BN-statistics
+epilogue, plus the separate BN statistics pass the epilogue replaces.
+Checks the GEMM against F.conv2d and the fused statistics against torch."""
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+torch.backends.cudnn.benchmark = True
+from mivod.ops import kernels as K  # noqa: E402
+
+nat = K.native()
+dev = torch.device("cuda")
+BS = int(os.environ.get("BS", 2048))
+# (H, Cin, Cout, launches per ResNet-50 step)
+SH = [(56, 64, 64, 1), (56, 256, 64, 2), (56, 64, 256, 4), (56, 256, 128, 1), (28, 512, 128, 3),
+      (28, 128, 512, 4), (28, 512, 256, 1), (14, 1024, 256, 5), (14, 256, 1024, 6),
+      (14, 1024, 512, 1), (7, 2048, 512, 2), (7, 512, 2048, 3)]
+
+
+def bench(fn, iters=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1000.0
+
+
+tot = [0.0] * 4
+for hw, cin, cout, cnt in SH:
+    M = BS * hw * hw
+    x = (torch.randn(BS, cin, hw, hw, device=dev) * 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, 1, 1, device=dev) / cin ** 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    a2 = x.permute(0, 2, 3, 1).reshape(M, cin)
+    w2 = w.reshape(cout, cin)
+    y = torch.empty(M, cout, device=dev, dtype=torch.bfloat16)
+    P = nat.gemm_partials(M, cout, cin)
+    part = torch.empty(P, 2, cout, device=dev)
+    shift = torch.zeros(cout, device=dev)
+    t_conv = bench(lambda: F.conv2d(x, w))
+    t_gemm = bench(lambda: nat.gemm_nt(a2, w2, y, None, None))
+    t_gst = bench(lambda: nat.gemm_nt(a2, w2, y, shift, part))
+    ref = F.conv2d(x, w).permute(0, 2, 3, 1).reshape(M, cout)
+    rm = torch.zeros(cout, device=dev)
+    rv = torch.ones(cout, device=dev)
+    yv = y.view(BS, hw, hw, cout).permute(0, 3, 1, 2)
+    t_stats = bench(lambda: nat.bn_stats(yv, None, None, rm, rv, 0.0, 1e-5))
+    nat.gemm_nt(a2, w2, y, shift, part)
+    torch.cuda.synchronize()
+    err = (y.float() - ref.float()).abs().max().item() / ref.float().abs().max().item()
+    s = part.sum(0)
+    yf = y.float()
+    es = ((s[0] - yf.sum(0)).abs().max() / yf.abs().sum(0).max()).item()
+    tot[0] += t_conv * cnt
+    tot[1] += t_gemm * cnt
+    tot[2] += t_gst * cnt
+    tot[3] += t_stats * cnt
+    gb = (M * cin + M * cout) * 2 / 1e9
+    print(f"M={M:8d} K={cin:4d} N={cout:4d} x{cnt}: conv2d {t_conv:8.1f} us | gemm {t_gemm:8.1f} us "
+          f"({gb / t_gemm * 1e6 / 1e3:5.2f} TB/s, {2 * M * cin * cout / t_gemm / 1e6:6.1f} TF) | "
+          f"gemm+stats {t_gst:8.1f} us | stats pass {t_stats:7.1f} us | rel err {err:.1e} "
+          f"stats err {es:.1e}", flush=True)
+    del x, y, a2, ref, yf
+    torch.cuda.empty_cache()
+print(f"per step: conv2d {tot[0] / 1e3:.2f} ms, gemm {tot[1] / 1e3:.2f} ms, gemm+stats "
+      f"{tot[2] / 1e3:.2f} ms, stats passes {tot[3] / 1e3:.2f} ms -> fused saving "
+      f"{(tot[0] + tot[3] - tot[2]) / 1e3:.2f} ms")
