@@ -827,6 +827,85 @@ void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
   mv_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, (int)N, (int)K, sp, pp, cur_stream());
 }
 
+int64_t gemm_bwd_partials(int64_t M, int64_t N, int64_t K, int64_t bn) {
+  return mv_gemm_bwd_partials(M, (int)N, (int)K, (int)bn);
+}
+
+// Data-gradient GEMM of a 1x1 conv fused with the BN+add+ReLU (mode 3) backward
+// reduce of the BN that produced the conv's input: dy = a . b^T, dz = mask ? dy + dy2
+// : 0 is written to dz, returns the fp32 [P, 2, N] partials (sum dz, sum dz (x - mean)).
+at::Tensor gemm_nt_bn_bwd(at::Tensor a, at::Tensor b, at::Tensor dz,
+                          c10::optional<at::Tensor> dy2, at::Tensor mask, at::Tensor x,
+                          at::Tensor vec, int64_t bn) {
+  for (const at::Tensor* t : {&a, &b, &dz, &x})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous(),
+                "gemm_nt_bn_bwd: A, B, dz, x must be contiguous bf16 GPU tensors");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm_nt_bn_bwd: A, B must be 2-D");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && M > 0, "gemm_nt_bn_bwd: shape mismatch");
+  TORCH_CHECK(dz.numel() == M * N && x.numel() == M * N, "gemm_nt_bn_bwd: dz/x must be [M, N]");
+  TORCH_CHECK(M * N < (int64_t(1) << 40) && N % 64 == 0, "gemm_nt_bn_bwd: bad size");
+  const int64_t P = gemm_bwd_partials(M, N, K, bn);
+  TORCH_CHECK(P > 0, "gemm_nt_bn_bwd: unsupported (K, N) — K must be 64, 128 or 256");
+  TORCH_CHECK(mask.is_cuda() && mask.scalar_type() == at::kByte && mask.is_contiguous() &&
+                  mask.numel() == M * (N / 8),
+              "gemm_nt_bn_bwd: mask must be the forward's [M, N/8] uint8 bitmask");
+  TORCH_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() &&
+                  vec.numel() == 4 * N, "gemm_nt_bn_bwd: saved stats must be fp32 [4, N]");
+  const void* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    const bool ok_layout = dy2->dim() == 4
+                               ? dy2->size(1) == N &&
+                                     dy2->is_contiguous(at::MemoryFormat::ChannelsLast)
+                               : dy2->is_contiguous();
+    TORCH_CHECK(dy2->is_cuda() && dy2->scalar_type() == at::kBFloat16 && ok_layout &&
+                    dy2->numel() == M * N,
+                "gemm_nt_bn_bwd: dy2 must be bf16 [M, N] (NHWC-contiguous)");
+    d2 = dy2->data_ptr();
+  }
+  for (const at::Tensor* t : {&b, &dz, &x, &mask, &vec})
+    TORCH_CHECK(t->device() == a.device(), "gemm_nt_bn_bwd: devices differ");
+  c10::DeviceGuard guard(a.device());
+  at::Tensor partial = at::empty({P, 2, N}, a.options().dtype(at::kFloat));
+  TORCH_CHECK(mv_gemm_nt_bn_bwd(a.data_ptr(), b.data_ptr(), dz.data_ptr(), M, (int)N, (int)K, d2,
+                                mask.data_ptr(), x.data_ptr(), vec[0].data_ptr<float>(),
+                                partial.data_ptr<float>(), (int)bn, cur_stream()),
+              "gemm_nt_bn_bwd: launch failed");
+  return partial;
+}
+
+// {dx, dgamma, dbeta} from a GEMM-epilogue reduce (gemm_nt_bn_bwd)
+std::vector<at::Tensor> bn_bwd_from_partials(at::Tensor dz, at::Tensor x, at::Tensor vec,
+                                             c10::optional<at::Tensor> gamma,
+                                             bool need_affine_grad, at::Tensor partial) {
+  int64_t C, C2;
+  const int64_t M = bn_check_act(x, "x", &C);
+  bn_check_act(dz, "dz", &C2);
+  TORCH_CHECK(dz.sizes() == x.sizes() && dz.strides() == x.strides(), "bn: dz layout mismatch");
+  TORCH_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() &&
+              vec.numel() == 4 * C, "bn: saved stats must be fp32 [4, C]");
+  TORCH_CHECK(partial.is_cuda() && partial.scalar_type() == at::kFloat && partial.is_contiguous() &&
+                  partial.dim() == 3 && partial.size(1) == 2 && partial.size(2) == C &&
+                  partial.size(0) > 0 && partial.size(0) < (int64_t(1) << 31),
+              "bn: partials must be fp32 [P, 2, C]");
+  c10::DeviceGuard guard(x.device());
+  at::Tensor work = at::empty({5, C}, x.options().dtype(at::kFloat));
+  at::Tensor dx = at::empty_like(x);
+  mv_bn_bwd_from_partials(dz.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C,
+                          vec[0].data_ptr<float>(), vec[1].data_ptr<float>(),
+                          opt_f32(gamma, C, "weight"), vec[2].data_ptr<float>(),
+                          vec[3].data_ptr<float>(), work[0].data_ptr<float>(),
+                          work[1].data_ptr<float>(), partial.data_ptr<float>(),
+                          (int)partial.size(0), work[2].data_ptr<float>(),
+                          work[3].data_ptr<float>(), work[4].data_ptr<float>(), cur_stream());
+  at::Tensor dg, db;
+  if (need_affine_grad) {
+    dg = work[0];
+    db = work[1];
+  }
+  return {dx, dg, db};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -869,5 +948,13 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
   m.def("pad_channels", &pad_channels, "NHWC zero channel padding C -> cout (<= 8)");
   m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics");
+  m.def("gemm_nt_bn_bwd", &gemm_nt_bn_bwd,
+        "1x1-conv data-gradient GEMM with the producing BN's add+ReLU backward reduce fused",
+        py::arg("a"), py::arg("b"), py::arg("dz"), py::arg("dy2"), py::arg("mask"), py::arg("x"),
+        py::arg("vec"), py::arg("bn") = 0);
+  m.def("gemm_bwd_partials", &gemm_bwd_partials, "partial rows of gemm_nt_bn_bwd (-1: unsupported)",
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bn") = 0);
+  m.def("bn_bwd_from_partials", &bn_bwd_from_partials,
+        "BN backward finalize + dx from GEMM-epilogue partials -> (dx, dgamma, dbeta)");
   m.def("gemm_partials", &gemm_partials, "row tiles (statistics partial rows) of gemm_nt");
 }

@@ -18,6 +18,12 @@ void mv_bn_fwd_from_partials(const void* x, const void* res, void* y, int64_t M,
                              float momentum, float eps, bool relu, const float* partial, int P,
                              float* save_mean, float* save_invstd, float* scale, float* bias,
                              hipStream_t st, void* mask = nullptr);
+// finalize + dx pass of a BN backward whose reduce ran in the producing GEMM's epilogue
+void mv_bn_bwd_from_partials(const void* dz, const void* x, void* dx, int64_t M, int C,
+                             const float* save_mean, const float* save_invstd,
+                             const float* gamma, const float* scale, const float* bias,
+                             float* dgamma, float* dbeta, const float* partial, int P, float* ca,
+                             float* cb, float* cc, hipStream_t st);
 
 void mv_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
                  const float* bias, bool relu, hipStream_t st, void* mask = nullptr);

@@ -746,3 +746,17 @@ void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const v
     default: launch_bwd_dx<0>((const __bf16*)dzp, xp, scale, bias, ca, cb, cc, dxp, M, C, st); break;
   }
 }
+
+// BN backward whose reduce pass ran inside the producing data-gradient GEMM
+// (mv_gemm_nt_bn_bwd): dz and its [P][2][C] partials (sum dz, sum dz (x - mean)) are
+// given, so only the finalize and the dx pass remain.
+void mv_bn_bwd_from_partials(const void* dz, const void* x, void* dx, int64_t M, int C,
+                             const float* save_mean, const float* save_invstd,
+                             const float* gamma, const float* scale, const float* bias,
+                             float* dgamma, float* dbeta, const float* partial, int P, float* ca,
+                             float* cb, float* cc, hipStream_t st) {
+  hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
+                     partial, P, M, C, save_mean, save_invstd, gamma, dgamma, dbeta, ca, cb, cc);
+  launch_bwd_dx<0>((const __bf16*)dz, (const __bf16*)x, scale, bias, ca, cb, cc, (__bf16*)dx, M, C,
+                   st);
+}

@@ -9,3 +9,13 @@ int64_t mv_gemm_partials(int64_t M, int N, int K);
 // partial != null: fused BN statistics of C around shift -> partial[ceil(M/BM)][2][N]
 void mv_gemm_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
                 const float* shift, float* partial, hipStream_t st);
+
+// Data-gradient GEMM with the following BN+add+ReLU backward reduce fused (EPI 2 of
+// the streaming kernel; K in {64, 128, 256} only — returns false otherwise):
+// dy = A . B^T (bf16-rounded), d = mask ? dy + dy2 : 0 -> DZ, partial[P][2][N] =
+// (sum d, sum d * (x - mean)) with P = mv_gemm_bwd_partials(M, N, K, bn); bn = the
+// column-tile width (0: default)
+int64_t mv_gemm_bwd_partials(int64_t M, int N, int K, int bn);
+bool mv_gemm_nt_bn_bwd(const void* A, const void* B, void* DZ, int64_t M, int N, int K,
+                       const void* dy2, const void* mask, const void* x, const float* mean,
+                       float* partial, int bn, hipStream_t st);

@@ -207,22 +207,64 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(
 // HBM-bound 1x1 convs of ResNet's early stages.  A persistent workgroup keeps its
 // [BN, K] filter slice in LDS for the whole kernel and streams 64-row tiles of A:
 // the next tile's 16-byte global loads are in flight (in registers) while the
-// current tile is multiplied and stored, and the fused statistics accumulate in
-// registers across ALL the tiles a workgroup processes — one cross-lane reduction
-// and one [2][BN] partial row per workgroup at the very end.  The 4 waves split
-// the BN columns (64 each), 64 rows x 64 columns per wave per tile.
+// current tile is multiplied and stored, and the fused epilogue's per-channel
+// sums accumulate in registers across ALL the tiles a workgroup processes — one
+// cross-lane reduction and one [2][BN] partial row per workgroup at the end.
+// The 4 waves split the BN columns, 64 rows x WTN columns per wave per tile.
+//
+// Column permutation: MFMA tile a's output row i (a filter row) is physical column
+// TN*4*(i >> 2) + 4a + (i & 3) of the wave's slice, so each lane ends up holding
+// 4*TN CONSECUTIVE channels of one output row: 16-byte stores, and 16-byte loads
+// for the epilogue operands.
+//
+// Epilogues (EPI):
+//   0  C = A . B^T
+//   1  + BN statistics of the bf16-rounded C around shift (forward, fused stats pass)
+//   2  BN+add+ReLU BACKWARD reduce fused into the data-gradient GEMM that produces
+//      the BN output's gradient dy: d = relu_mask ? bf16(dy) + dy2 : 0 is written
+//      (dz, the residual branch's gradient) instead of dy, and the partials are
+//      (sum d, sum d * (x - mean)) — exactly mv_bn.hip's bwd_reduce_kernel<3>
+//      (x = the BN input, mask = the forward's bitmask, dy2 = the shortcut gradient).
 // ---------------------------------------------------------------------------
-template <int K, int BN, bool STATS>
+struct BwdEpi {
+  const __bf16* dy2;      // [M, N] second gradient stream (shortcut), may be null
+  const uint8_t* mask;    // [M, N/8] bitmask of the forward output > 0
+  const __bf16* x;        // [M, N] BN input
+  const float* mean;      // [N] saved mean
+};
+
+// raw 16-/8-byte loads of NC consecutive bf16 (issued early, unpacked in the epilogue)
+template <int NC>
+__device__ __forceinline__ void ld_raw(const __bf16* p, uint32_t (&r)[NC / 2]) {
+  if constexpr (NC == 4) {
+    const u32x2 w = *reinterpret_cast<const u32x2*>(p);
+    r[0] = w[0];
+    r[1] = w[1];
+  } else {
+#pragma unroll
+    for (int h = 0; h < NC / 8; ++h) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(p + 8 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[4 * h + j] = w[j];
+    }
+  }
+}
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+template <int K, int BN, int EPI>
 __global__ __launch_bounds__(256) void gemm_stream_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
     int64_t M, int N, int ntn, int64_t ntm, const float* __restrict__ shift,
-    float* __restrict__ partial) {
+    float* __restrict__ partial, BwdEpi be) {
   constexpr int BM = 64;
   constexpr int KCH = K / 8;                 // 16-byte chunks per row
   constexpr int A_CH = BM * KCH / 256;       // A chunks per thread per tile
   constexpr int W_CH = BN * KCH / 256;
   constexpr int WTN = BN / 4;                // columns per wave
   constexpr int TN = WTN / 16, TM = BM / 16;
+  constexpr int NC = 4 * TN;                 // consecutive channels per lane
   __shared__ __attribute__((aligned(16))) __bf16 smem[(BN + BM) * K];
   __bf16* Ws = smem;
   __bf16* As = smem + BN * K;
@@ -234,6 +276,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
   const int nt = t % ntn;
   const int64_t stream = t / ntn, nstreams = gridDim.x / ntn;
   const int n0 = nt * BN;
+  const int cbase = n0 + wn * WTN + NC * g;  // this lane's first output channel
 
   // filter slice -> LDS (once)
 #pragma unroll
@@ -253,18 +296,34 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       ra[i] = *reinterpret_cast<const u32x4*>(A + gm * K + ch * 8);
     }
   };
-  float sh[TN][4], s1[TN][4], s2[TN][4];
+  float sh[NC], s1[NC], s2[NC];
 #pragma unroll
-  for (int a = 0; a < TN; ++a)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      sh[a][r] = (STATS && shift) ? shift[n0 + wn * WTN + a * 16 + 4 * g + r] : 0.f;
-      s1[a][r] = 0.f;
-      s2[a][r] = 0.f;
-    }
+  for (int j = 0; j < NC; ++j) {
+    sh[j] = 0.f;
+    if (EPI == 1 && shift) sh[j] = shift[cbase + j];
+    if (EPI == 2) sh[j] = be.mean[cbase + j];
+    s1[j] = 0.f;
+    s2[j] = 0.f;
+  }
   int64_t mt = stream;
   if (mt < ntm) gload(mt);
   for (; mt < ntm; mt += nstreams) {
+    // EPI 2: this tile's epilogue operands, in flight during the MFMA work
+    uint32_t e2[EPI == 2 ? TM : 1][NC / 2], ex[EPI == 2 ? TM : 1][NC / 2];
+    uint32_t em[EPI == 2 ? TM : 1];
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int b = 0; b < TM; ++b) {
+        int64_t row = mt * BM + b * 16 + rl;
+        row = row < M ? row : M - 1;
+        if (be.dy2) ld_raw<NC>(be.dy2 + row * N + cbase, e2[b]);
+        ld_raw<NC>(be.x + row * N + cbase, ex[b]);
+        const uint8_t* mp = be.mask + row * (N / 8) + cbase / 8;
+        if constexpr (NC == 4) em[b] = (uint32_t)mp[0] >> (cbase & 7);
+        else if constexpr (NC == 8) em[b] = mp[0];
+        else em[b] = *reinterpret_cast<const uint16_t*>(mp);
+      }
+    }
     __syncthreads();                                   // previous tile's LDS reads done
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
@@ -284,7 +343,8 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       bf16x8 wf[TN], af[TM];
 #pragma unroll
       for (int a = 0; a < TN; ++a)
-        wf[a] = *reinterpret_cast<const bf16x8*>(Ws + sw(wn * WTN + a * 16 + rl, ch));
+        wf[a] = *reinterpret_cast<const bf16x8*>(
+            Ws + sw(wn * WTN + NC * (rl >> 2) + 4 * a + (rl & 3), ch));
 #pragma unroll
       for (int b = 0; b < TM; ++b)
         af[b] = *reinterpret_cast<const bf16x8*>(As + sw(b * 16 + rl, ch));
@@ -297,47 +357,72 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
 #pragma unroll
     for (int b = 0; b < TM; ++b) {
       const int64_t row = m0 + b * 16 + rl;
-      if (row < M) {
+      if (row >= M) continue;
+      uint32_t pk[2 * TN];
 #pragma unroll
-        for (int a = 0; a < TN; ++a) {
-          const f32x4v v = acc[a][b];
-          const uint32_t p0 = cvt_pk_bf16(v[0], v[1]), p1 = cvt_pk_bf16(v[2], v[3]);
-          u32x2 o = {p0, p1};
-          *reinterpret_cast<u32x2*>(C + row * N + n0 + wn * WTN + a * 16 + 4 * g) = o;
-          if (STATS) {
-            const float q[4] = {__uint_as_float(p0 << 16), __uint_as_float(p0 & 0xffff0000u),
-                                __uint_as_float(p1 << 16), __uint_as_float(p1 & 0xffff0000u)};
+      for (int a = 0; a < TN; ++a) {
+        pk[2 * a] = cvt_pk_bf16(acc[a][b][0], acc[a][b][1]);
+        pk[2 * a + 1] = cvt_pk_bf16(acc[a][b][2], acc[a][b][3]);
+      }
+      float v[NC];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float d = q[r] - sh[a][r];
-              s1[a][r] += d;
-              s2[a][r] += d * d;
-            }
+      for (int j = 0; j < NC / 2; ++j) {
+        v[2 * j] = __uint_as_float(pk[j] << 16);
+        v[2 * j + 1] = __uint_as_float(pk[j] & 0xffff0000u);
+      }
+      if (EPI == 1) {
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const float d = v[j] - sh[j];
+          s1[j] += d;
+          s2[j] += d * d;
+        }
+      }
+      if constexpr (EPI == 2) {
+        if (be.dy2) {
+#pragma unroll
+          for (int j = 0; j < NC / 2; ++j) {
+            v[2 * j] += bf_lo(e2[b][j]);
+            v[2 * j + 1] += bf_hi(e2[b][j]);
           }
         }
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const float xv = (j & 1) ? bf_hi(ex[b][j >> 1]) : bf_lo(ex[b][j >> 1]);
+          const float d = ((em[b] >> j) & 1u) ? v[j] : 0.f;
+          v[j] = d;
+          s1[j] += d;
+          s2[j] += d * (xv - sh[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < NC / 2; ++j) pk[j] = cvt_pk_bf16(v[2 * j], v[2 * j + 1]);
+      }
+      __bf16* cp = C + row * N + cbase;
+      if constexpr (NC == 4) {
+        *reinterpret_cast<u32x2*>(cp) = u32x2{pk[0], pk[1]};
+      } else {
+#pragma unroll
+        for (int h = 0; h < NC / 8; ++h)
+          *reinterpret_cast<u32x4*>(cp + 8 * h) =
+              u32x4{pk[4 * h], pk[4 * h + 1], pk[4 * h + 2], pk[4 * h + 3]};
       }
     }
   }
-  if (!STATS) return;
+  if (EPI == 0) return;
 #pragma unroll
-  for (int a = 0; a < TN; ++a)
+  for (int j = 0; j < NC; ++j) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        s1[a][r] += __shfl_xor(s1[a][r], o, kWave);
-        s2[a][r] += __shfl_xor(s2[a][r], o, kWave);
-      }
+    for (int o = 1; o < 16; o <<= 1) {
+      s1[j] += __shfl_xor(s1[j], o, kWave);
+      s2[j] += __shfl_xor(s2[j], o, kWave);
     }
+  }
   if (rl == 0 && stream < ntm) {
 #pragma unroll
-    for (int a = 0; a < TN; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = n0 + wn * WTN + a * 16 + 4 * g + r;
-        partial[(stream * 2 + 0) * N + c] = s1[a][r];
-        partial[(stream * 2 + 1) * N + c] = s2[a][r];
-      }
+    for (int j = 0; j < NC; ++j) {
+      partial[(stream * 2 + 0) * N + cbase + j] = s1[j];
+      partial[(stream * 2 + 1) * N + cbase + j] = s2[j];
+    }
   }
 }
 
@@ -378,12 +463,12 @@ static bool stream_cfg(int K, int N, int* bn) {
   return false;
 }
 
-template <int K, int BN, bool STATS>
+template <int K, int BN, int EPI>
 static int64_t streams_for(int64_t M, int N) {
   static int per = [] {
     int v = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &v, (const void*)&mv::gemm::gemm_stream_kernel<K, BN, STATS>, 256, 0) != hipSuccess ||
+            &v, (const void*)&mv::gemm::gemm_stream_kernel<K, BN, EPI>, 256, 0) != hipSuccess ||
         v < 1)
       v = 1;
     return v;
@@ -398,18 +483,25 @@ static int64_t streams_for(int64_t M, int N) {
 
 template <int K, int BN>
 static void launch_stream(const __bf16* a, const __bf16* b, __bf16* c, int64_t M, int N,
-                          const float* shift, float* partial, hipStream_t st) {
+                          const float* shift, float* partial, const mv::gemm::BwdEpi* be,
+                          hipStream_t st) {
   using namespace mv::gemm;
   const int ntn = N / BN;
   const int64_t ntm = (M + 63) / 64;
-  if (partial) {
-    const dim3 grid((unsigned)(streams_for<K, BN, true>(M, N) * ntn));
-    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, true>), grid, dim3(256), 0, st, a, b, c, M, N,
-                       ntn, ntm, shift, partial);
+  BwdEpi e{};
+  if (be) {
+    e = *be;
+    const dim3 grid((unsigned)(streams_for<K, BN, 2>(M, N) * ntn));
+    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 2>), grid, dim3(256), 0, st, a, b, c, M, N,
+                       ntn, ntm, shift, partial, e);
+  } else if (partial) {
+    const dim3 grid((unsigned)(streams_for<K, BN, 1>(M, N) * ntn));
+    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 1>), grid, dim3(256), 0, st, a, b, c, M, N,
+                       ntn, ntm, shift, partial, e);
   } else {
-    const dim3 grid((unsigned)(streams_for<K, BN, false>(M, N) * ntn));
-    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, false>), grid, dim3(256), 0, st, a, b, c, M, N,
-                       ntn, ntm, shift, partial);
+    const dim3 grid((unsigned)(streams_for<K, BN, 0>(M, N) * ntn));
+    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 0>), grid, dim3(256), 0, st, a, b, c, M, N,
+                       ntn, ntm, shift, partial, e);
   }
 }
 
@@ -421,7 +513,7 @@ int64_t mv_gemm_partials(int64_t M, int N, int K) {
   int bn;
   if (stream_cfg(K, N, &bn)) {
 #define MV_P(KK, BB) \
-    if (K == KK && bn == BB) return streams_for<KK, BB, true>(M, N);
+    if (K == KK && bn == BB) return streams_for<KK, BB, 1>(M, N);
     MV_STREAM_CASES(MV_P)
 #undef MV_P
   }
@@ -438,7 +530,7 @@ void mv_gemm_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
   int bn;
   if (stream_cfg(K, N, &bn)) {
 #define MV_L(KK, BB) \
-    if (K == KK && bn == BB) { launch_stream<KK, BB>(a, b, c, M, N, shift, partial, st); return; }
+    if (K == KK && bn == BB) { launch_stream<KK, BB>(a, b, c, M, N, shift, partial, nullptr, st); return; }
     MV_STREAM_CASES(MV_L)
 #undef MV_L
   }
@@ -448,4 +540,47 @@ void mv_gemm_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
     launch<128, 128, 2, 2>(a, b, c, M, N, K, shift, partial, st);
   else
     launch<256, 64, 4, 1>(a, b, c, M, N, K, shift, partial, st);
+}
+
+// column-tile width of the EPI 2 kernel (req > 0 forces one).  The widest tile wins
+// despite 1 wave/SIMD: its epilogue operands are prefetched a whole tile ahead, and the
+// A operand is read once (scripts/micro_gemm1x1.py bwd sweep: K64N256 bn256 1878 us vs
+// bn128 2245 / bn64 3415; K256N1024 bn128 751 vs bn64 1090)
+static bool bwd_cfg(int K, int N, int req, int* bn) {
+  if (K != 64 && K != 128 && K != 256) return false;
+  int b = req > 0 ? req : (K == 256 ? 128 : 256);
+  if (K == 256 && b > 128) b = 128;
+  while (b > 64 && N % b) b >>= 1;
+  if (b != 64 && b != 128 && b != 256) return false;
+  if (N % b) return false;
+  *bn = b;
+  return true;
+}
+
+// number of partial rows of mv_gemm_nt_bn_bwd (the EPI 2 kernel's persistent grid)
+int64_t mv_gemm_bwd_partials(int64_t M, int N, int K, int req_bn) {
+  int bn;
+  if (!bwd_cfg(K, N, req_bn, &bn)) return -1;
+#define MV_PB(KK, BB) \
+  if (K == KK && bn == BB) return streams_for<KK, BB, 2>(M, N);
+  MV_STREAM_CASES(MV_PB)
+#undef MV_PB
+  return -1;
+}
+
+bool mv_gemm_nt_bn_bwd(const void* A, const void* B, void* DZ, int64_t M, int N, int K,
+                       const void* dy2, const void* mask, const void* x, const float* mean,
+                       float* partial, int req_bn, hipStream_t st) {
+  using namespace mv::gemm;
+  int bn;
+  if (!bwd_cfg(K, N, req_bn, &bn)) return false;
+  BwdEpi e{(const __bf16*)dy2, (const uint8_t*)mask, (const __bf16*)x, mean};
+  const __bf16* a = (const __bf16*)A;
+  const __bf16* b = (const __bf16*)B;
+  __bf16* c = (__bf16*)DZ;
+#define MV_LB(KK, BB) \
+  if (K == KK && bn == BB) { launch_stream<KK, BB>(a, b, c, M, N, nullptr, partial, &e, st); return true; }
+  MV_STREAM_CASES(MV_LB)
+#undef MV_LB
+  return false;
 }

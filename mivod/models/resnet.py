@@ -63,9 +63,17 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
+        # conv_bn: a qualifying 1x1 conv computes its BN's statistics in the GEMM
+        # epilogue (mivod.ops.conv), so the BN skips its statistics pass; conv1's data
+        # gradient also runs the backward reduce of the BN that produced x
+        out = conv_bn(self.conv1, self.bn1, x, relu=True)
+        out = self.bn2(self.conv2(out), relu=True)
         # the shortcut's gradient is added inside the backward of the op that
         # produced x (mivod.ops.bn.tap), not by a separate autograd add; a strided
-        # 1x1 shortcut conv hands it over at its output resolution (downsample_tap)
+        # 1x1 shortcut conv hands it over at its output resolution (downsample_tap).
+        # The tap is recorded AFTER the main branch so that autograd (which runs the
+        # most recently recorded ready node first) parks the shortcut gradient before
+        # conv1's backward, which then finds it for the fused reduce.
         if self.downsample is None:
             identity = tap(x)
         else:
@@ -74,10 +82,6 @@ class Bottleneck(nn.Module):
                 identity = conv_bn(conv, rest[0], tap(x))
             else:
                 identity = rest(downsample_tap(x, conv))
-        # conv_bn: a qualifying 1x1 conv computes its BN's statistics in the GEMM
-        # epilogue (mivod.ops.conv.conv1x1_stats), so the BN skips its statistics pass
-        out = conv_bn(self.conv1, self.bn1, x, relu=True)
-        out = self.bn2(self.conv2(out), relu=True)
         # fused: relu(bn3(conv3(out)) + identity) in one pass (mivod.ops.bn)
         return conv_bn(self.conv3, self.bn3, out, relu=True, residual=identity)
 

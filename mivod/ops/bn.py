@@ -47,12 +47,17 @@ class GradSlot:
     (1 extra read).  Autograd still orders the producer after the tap: a None
     gradient satisfies the dependency edge.
     """
-    __slots__ = ("grad", "stride", "full_shape")
+    __slots__ = ("grad", "stride", "full_shape", "bn", "pending")
 
     def __init__(self):
         self.grad = None
         self.stride = 1          # > 1: grad is on the stride-s grid (downsample_tap)
         self.full_shape = None   # the tapped output's shape when stride > 1
+        # (x, mask, vec) of the producing mode-3 BN, for a consumer conv whose data
+        # gradient GEMM runs this BN's backward reduce (ops.conv._Conv1x1BN) ...
+        self.bn = None
+        # ... and its result (dz, partials), consumed by the BN backward
+        self.pending = None
 
     def take(self):
         g, self.grad = self.grad, None
@@ -173,13 +178,35 @@ class _BNActTrain(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.slot = slot
         ctx.save_for_backward(x, keep, vec, weight)
+        if slot is not None and mode == 3:
+            slot.bn = (x, keep, vec)
+            ctx.set_materialize_grads(False)    # dy is None when a consumer took the reduce
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, y, vec, weight = ctx.saved_tensors
-        dy = _cl(dy)
         need_affine = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        pending = None
+        if ctx.slot is not None:
+            ctx.slot.bn = None
+            pending, ctx.slot.pending = ctx.slot.pending, None
+        if pending is not None:
+            # the consumer conv's dgrad GEMM already produced dz (masked, shortcut
+            # gradient included) and the reduce partials (ops.conv._Conv1x1BN)
+            dz, part = pending
+            assert ctx.slot.grad is None, "a tapped output has one shortcut consumer"
+            if dy is None:
+                dx, dg, db = K.native().bn_bwd_from_partials(dz, x, vec, weight, need_affine, part)
+            else:   # a further consumer: d = mask ? dy + dz : 0 (dz is already masked)
+                dx, dg, db, dz = K.native().bn_bwd(3, _cl(dy), x, y, vec, weight, need_affine,
+                                                   dz, 1)
+            return (dx if ctx.needs_input_grad[0] else None,
+                    dg if ctx.needs_input_grad[1] else None,
+                    db if ctx.needs_input_grad[2] else None,
+                    None, None, None, None, None, dz if ctx.needs_input_grad[8] else None,
+                    None, None)
+        dy = _cl(dy) if dy is not None else torch.zeros_like(x)
         dy2, s2 = None, 1
         if ctx.slot is not None:
             dy2, s2 = ctx.slot.take_strided() if ctx.mode >= 2 else (ctx.slot.take(), 1)
@@ -365,10 +392,14 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = Fa
             residual=None) -> torch.Tensor:
     """``bn(conv(x), residual, relu)`` with the BN statistics computed inside the
     1x1 conv's GEMM epilogue when the conv qualifies (ops.conv.stats_fusable) and
-    the BN is training with running statistics; the plain composition otherwise."""
-    from .conv import conv1x1_stats, stats_fusable
-    if (bn.training and bn.track_running_stats and bn.running_mean is not None
-            and _fusable(x, bn.weight) and stats_fusable(conv, x)):
-        y, part = conv1x1_stats(conv, x, bn.running_mean)
-        return bn(y, residual=residual, relu=relu, stats=part)
+    the BN is training with running statistics, and with x's producer BN backward
+    reduce run in this conv's data-gradient GEMM when x is a fused BN+add+ReLU output
+    (ops.conv.bwd_fusable); the plain composition otherwise."""
+    from .conv import bwd_fusable, conv1x1_bn, stats_fusable
+    fwd = (bn.training and bn.track_running_stats and bn.running_mean is not None
+           and _fusable(x, bn.weight) and stats_fusable(conv, x))
+    slot = bwd_fusable(conv, x)
+    if fwd or slot is not None:
+        y, part = conv1x1_bn(conv, x, bn.running_mean if fwd else None, fwd, slot)
+        return bn(y, residual=residual, relu=relu, stats=part if fwd else None)
     return bn(conv(x), residual=residual, relu=relu)

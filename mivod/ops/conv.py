@@ -24,7 +24,9 @@ the FOLLOWING BatchNorm's statistics computed in the GEMM epilogue — the BN's
 separate statistics pass over the conv output disappears.  Used only where the
 GEMM is at least as fast as MIOpen's kernel (scripts/micro_gemm1x1.py,
 profiles/r2_gemm1x1_fused_stats.md); its backward is the same forward-conv dgrad
-+ MIOpen wgrad as above.
++ MIOpen wgrad as above — or, when the conv's input is a fused BN+add+ReLU output
+(every non-entry ResNet bottleneck), the data gradient is mivod's GEMM with that
+BN's backward reduce in the epilogue (``_Conv1x1BN``, ``MIVOD_CONV_BN_BWD_FUSE``).
 """
 from __future__ import annotations
 
@@ -73,26 +75,44 @@ def _eligible(m: nn.Conv2d, x: torch.Tensor) -> bool:
             and x.is_contiguous(memory_format=torch.channels_last))
 
 
-class _Conv1x1Stats(torch.autograd.Function):
-    """y = conv1x1(x, w) via mv_gemm (NHWC GEMM) + [P, 2, Cout] BN statistics
-    partials of y around ``shift`` (non-differentiable side output)."""
+class _Conv1x1BN(torch.autograd.Function):
+    """1x1 stride-1 conv feeding a BatchNorm, with two optional fusions.
+
+    Forward (``gemm``): y = conv1x1(x, w) via mv_gemm (NHWC GEMM) + [P, 2, Cout] BN
+    statistics partials of y around ``shift`` (non-differentiable side output); else
+    MIOpen's forward and an empty partial tensor.
+
+    Backward (``slot``): when x is the output of a fused BN+add+ReLU (ops.bn, mode 3)
+    whose shortcut gradient is already parked in its GradSlot, the data gradient runs
+    as mv_gemm's streaming kernel with THAT BN's backward reduce in the epilogue:
+    dz = mask ? dx + dy_shortcut : 0 is written instead of dx, the partials
+    (sum dz, sum dz (x_bn - mean)) ride along, and both are handed to the BN through
+    the slot (``slot.pending``) while autograd receives None for x.  The BN backward
+    then skips its reduce pass (one full read of dx, dy2, x_bn and a write of dz).
+    """
 
     @staticmethod
-    def forward(ctx, x, w, shift):
+    def forward(ctx, x, w, shift, gemm, slot):
         from . import kernels as K
-        nat = K.native()
         n, cin, h, wd = x.shape
         cout = w.shape[0]
-        m = n * h * wd
-        a = x.permute(0, 2, 3, 1).reshape(m, cin)            # NHWC view, no copy
-        b = w.permute(0, 2, 3, 1).reshape(cout, cin)
-        yf = torch.empty(m, cout, dtype=x.dtype, device=x.device)
-        part = torch.empty(nat.gemm_partials(m, cout, cin), 2, cout, dtype=torch.float32,
-                           device=x.device)
-        nat.gemm_nt(a, b, yf, shift, part)
+        if gemm:
+            nat = K.native()
+            m = n * h * wd
+            a = x.permute(0, 2, 3, 1).reshape(m, cin)            # NHWC view, no copy
+            b = w.permute(0, 2, 3, 1).reshape(cout, cin)
+            yf = torch.empty(m, cout, dtype=x.dtype, device=x.device)
+            part = torch.empty(nat.gemm_partials(m, cout, cin), 2, cout, dtype=torch.float32,
+                               device=x.device)
+            nat.gemm_nt(a, b, yf, shift, part)
+            y = yf.view(n, h, wd, cout).permute(0, 3, 1, 2)
+        else:
+            y = F.conv2d(x, w)
+            part = torch.empty(0, dtype=torch.float32, device=x.device)
         ctx.save_for_backward(x, w)
+        ctx.slot = slot
         ctx.mark_non_differentiable(part)
-        return yf.view(n, h, wd, cout).permute(0, 3, 1, 2), part
+        return y, part
 
     @staticmethod
     def backward(ctx, dy, _dpart):
@@ -100,11 +120,25 @@ class _Conv1x1Stats(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = F.conv2d(dy, _transposed_filter(w))
+            slot, ctx.slot = ctx.slot, None
+            if (slot is not None and slot.bn is not None and slot.grad is not None
+                    and slot.stride == 1 and slot.pending is None):
+                from . import kernels as K
+                n, cin, h, wd = x.shape
+                cout, m = w.shape[0], n * h * wd
+                xb, mask, vec = slot.bn
+                dz = torch.empty_like(x)
+                part = K.native().gemm_nt_bn_bwd(
+                    dy.permute(0, 2, 3, 1).reshape(m, cout), w.reshape(cout, cin).t().contiguous(),
+                    dz.permute(0, 2, 3, 1).reshape(m, cin), slot.take(), mask,
+                    xb.permute(0, 2, 3, 1).reshape(m, cin), vec)
+                slot.pending = (dz, part)
+            else:
+                dx = F.conv2d(dy, _transposed_filter(w))
         if ctx.needs_input_grad[1]:
             _, dw, _ = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])
-        return dx, dw, None
+        return dx, dw, None, None, None
 
 
 def stats_fusable(m: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -117,9 +151,27 @@ def stats_fusable(m: nn.Conv2d, x: torch.Tensor) -> bool:
             and (cin in (64, 128, 256) or (cin == 512 and cout == 128)))
 
 
+def bwd_fusable(m: nn.Conv2d, x: torch.Tensor):
+    """GradSlot of x's producer when this 1x1 conv's data gradient can carry that
+    producer's BN backward reduce (Cout = the GEMM's K in {64, 128, 256}); else None."""
+    slot = getattr(x, "_mv_slot", None)
+    if (slot is None or getattr(slot, "bn", None) is None
+            or os.environ.get("MIVOD_CONV_BN_BWD_FUSE", "1") == "0"
+            or not (torch.is_grad_enabled() and x.requires_grad) or not _eligible(m, x)
+            or tuple(m.kernel_size) != (1, 1) or m.out_channels not in (64, 128, 256)
+            or m.in_channels % 64 != 0):
+        return None
+    return slot
+
+
+def conv1x1_bn(m: nn.Conv2d, x: torch.Tensor, shift, gemm: bool, slot):
+    """(y, partial) — see _Conv1x1BN; ``shift`` is the BN's running mean (gemm only)."""
+    return _Conv1x1BN.apply(x, m.weight, shift, gemm, slot)
+
+
 def conv1x1_stats(m: nn.Conv2d, x: torch.Tensor, shift):
-    """(y, partial) — see _Conv1x1Stats; ``shift`` is the BN's running mean."""
-    return _Conv1x1Stats.apply(x, m.weight, shift)
+    """(y, partial) of the GEMM forward with fused statistics."""
+    return _Conv1x1BN.apply(x, m.weight, shift, True, None)
 
 
 class Conv2d(nn.Conv2d):

@@ -77,3 +77,56 @@ for hw, cin, cout, cnt in SH:
 print(f"per step: conv2d {tot[0] / 1e3:.2f} ms, gemm {tot[1] / 1e3:.2f} ms, gemm+stats "
       f"{tot[2] / 1e3:.2f} ms, stats passes {tot[3] / 1e3:.2f} ms -> fused saving "
       f"{(tot[0] + tot[3] - tot[2]) / 1e3:.2f} ms")
+
+# ---- backward: conv1 data gradient + the previous block's BN(+add+ReLU) backward
+# (dgrad K = conv1's Cout, N = its Cin); unfused = MIOpen forward-conv dgrad + the
+# 3-kernel mode-3 BN backward; fused = gemm_nt_bn_bwd + finalize/dx from partials
+BW = [(56, 64, 256, 2), (28, 128, 512, 3), (14, 256, 1024, 5)]
+tb = [0.0, 0.0]
+for hw, k, n, cnt in BW:
+    M = BS * hw * hw
+    dy = (torch.randn(BS, k, hw, hw, device=dev)).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    wt = (torch.randn(n, k, 1, 1, device=dev) / k ** 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    xb = torch.randn(BS, n, hw, hw, device=dev).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    res = torch.randn_like(xb)
+    dy2 = torch.randn_like(xb)
+    gm = torch.ones(n, device=dev)
+    bt = torch.zeros(n, device=dev)
+    _, vec, mask = nat.bn_fwd_train_mask(xb, gm, bt, torch.zeros(n, device=dev),
+                                         torch.ones(n, device=dev), 0.1, 1e-5, res)
+    a2 = dy.permute(0, 2, 3, 1).reshape(M, k)
+    w2 = wt.reshape(n, k)
+    dz = torch.empty_like(xb)
+    dz2 = dz.permute(0, 2, 3, 1).reshape(M, n)
+    x2 = xb.permute(0, 2, 3, 1).reshape(M, n)
+
+    def unfused():
+        g = F.conv2d(dy, wt)
+        nat.bn_bwd(3, g, xb, mask, vec, gm, True, dy2, 1)
+
+    def fused():
+        p = nat.gemm_nt_bn_bwd(a2, w2, dz2, dy2, mask, x2, vec)
+        nat.bn_bwd_from_partials(dz, xb, vec, gm, True, p)
+
+    def fused_gemm(bn=0):
+        nat.gemm_nt_bn_bwd(a2, w2, dz2, dy2, mask, x2, vec, bn)
+
+    tu = bench(unfused)
+    tf = bench(fused)
+    tg = bench(fused_gemm)
+    sweep = " ".join(f"bn{b}={bench(lambda: fused_gemm(b)):.0f}" for b in (64, 128, 256)
+                     if nat.gemm_bwd_partials(M, n, k, b) > 0)
+    tc = bench(lambda: F.conv2d(dy, wt))
+    tb[0] += tu * cnt
+    tb[1] += tf * cnt
+    gb = (M * k + 4 * M * n) * 2 / 1e9
+    print(f"bwd M={M:8d} K={k:4d} N={n:4d} x{cnt}: dgrad conv {tc:8.1f} us, dgrad+bn_bwd "
+          f"{tu:8.1f} us | fused gemm {tg:8.1f} us ({gb / tg * 1e6 / 1e3:5.2f} TB/s), "
+          f"fused total {tf:8.1f} us [{sweep}]", flush=True)
+    del dy, xb, res, dy2, dz, mask
+    torch.cuda.empty_cache()
+print(f"bwd per step: unfused {tb[0] / 1e3:.2f} ms, fused {tb[1] / 1e3:.2f} ms -> saving "
+      f"{(tb[0] - tb[1]) / 1e3:.2f} ms")

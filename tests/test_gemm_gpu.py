@@ -89,7 +89,7 @@ def test_conv_bn_fused_matches_unfused(cuda, monkeypatch):
 
 
 def test_resnet_uses_gemm_stats_path(cuda):
-    """The bottleneck's qualifying 1x1 convs run through _Conv1x1Stats."""
+    """The bottleneck's qualifying 1x1 convs run through _Conv1x1BN."""
     from mivod.models.resnet import ResNet, to_mixed_bf16
     m = to_mixed_bf16(ResNet((1, 1, 1, 1), num_classes=10)).to(cuda)
     x = torch.rand(2, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(
@@ -103,4 +103,126 @@ def test_resnet_uses_gemm_stats_path(cuda):
         seen.add(f)
         names.add(type(f).__name__)
         stack.extend(nf for nf, _ in f.next_functions)
-    assert any("Conv1x1Stats" in n for n in names), names
+    assert any("Conv1x1BN" in n for n in names), names
+
+
+def _unpack_mask(mask, N):
+    bits = torch.arange(8, device=mask.device)
+    return ((mask.long().unsqueeze(-1) >> bits) & 1).reshape(mask.shape[0], N).bool()
+
+
+@pytest.mark.parametrize("K,N", [(64, 64), (64, 256), (128, 128), (128, 512), (256, 64),
+                                 (256, 1024)])
+@pytest.mark.parametrize("M", [1, 64 * 3 + 5, 4096 + 17])
+@pytest.mark.parametrize("with_dy2", [True, False])
+def test_gemm_nt_bn_bwd_matches_fp32(cuda, M, K, N, with_dy2):
+    """dz = mask ? bf16(a . b^T) + dy2 : 0 and the (sum dz, sum dz (x - mean)) partials."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(M + 3 * K + N)
+    a = torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).to(torch.bfloat16)
+    x = torch.randn(M, N, device=cuda, generator=g).to(torch.bfloat16)
+    vec = torch.randn(4, N, device=cuda, generator=g)
+    mask = torch.randint(0, 256, (M, N // 8), device=cuda, generator=g, dtype=torch.int32).to(
+        torch.uint8)
+    dy2 = (torch.randn(M, N, device=cuda, generator=g).to(torch.bfloat16)
+           if with_dy2 else None)
+    dz = torch.full((M, N), float("nan"), device=cuda).to(torch.bfloat16)
+    part = nat.gemm_nt_bn_bwd(a, b, dz, dy2, mask, x, vec)
+    assert part.shape == (nat.gemm_bwd_partials(M, N, K), 2, N)
+    dyb = (a.float() @ b.float().t()).to(torch.bfloat16).float()
+    d = dyb + (dy2.float() if with_dy2 else 0.0)
+    d = torch.where(_unpack_mask(mask, N), d, torch.zeros_like(d))
+    torch.testing.assert_close(dz.float(), d, rtol=2e-2, atol=2e-2)
+    assert torch.isfinite(part).all()
+    s = part.sum(0)
+    torch.testing.assert_close(s[0], d.sum(0), rtol=1e-2, atol=1e-2 * (M ** 0.5))
+    torch.testing.assert_close(s[1], (d * (x.float() - vec[0])).sum(0), rtol=1e-2,
+                               atol=3e-2 * (M ** 0.5))
+    assert (dz.float()[~_unpack_mask(mask, N)] == 0).all()
+
+
+def test_gemm_nt_bn_bwd_rejects_unsupported(cuda):
+    nat = _nat()
+    M, K, N = 64, 512, 128          # K = 512: no streaming kernel
+    z = lambda *s: torch.zeros(*s, device=cuda, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        nat.gemm_nt_bn_bwd(z(M, K), z(N, K), z(M, N), None,
+                           torch.zeros(M, N // 8, device=cuda, dtype=torch.uint8), z(M, N),
+                           torch.zeros(4, N, device=cuda))
+    with pytest.raises(RuntimeError):   # mask of the wrong size
+        nat.gemm_nt_bn_bwd(z(M, 64), z(N, 64), z(M, N), None,
+                           torch.zeros(M, N // 16, device=cuda, dtype=torch.uint8), z(M, N),
+                           torch.zeros(4, N, device=cuda))
+
+
+def test_bn_bwd_from_partials_matches_bn_bwd(cuda):
+    """finalize + dx from GEMM-epilogue partials == the mode-3 BN backward on the same dy."""
+    from mivod.ops.bn import BatchNorm2d
+    nat = _nat()
+    torch.manual_seed(1)
+    n, c, h, w, k = 8, 256, 14, 14, 64
+    bn = BatchNorm2d(c).to(cuda)
+    xin = torch.randn(n, c, h, w, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    res = torch.randn_like(xin)
+    _, vec, mask = nat.bn_fwd_train_mask(xin, bn.weight, bn.bias, bn.running_mean,
+                                         bn.running_var, 0.1, 1e-5, res)
+    m = n * h * w
+    a = torch.randn(m, k, device=cuda).to(torch.bfloat16)
+    wt = (torch.randn(c, k, device=cuda) / 8).to(torch.bfloat16)
+    dy2 = torch.randn_like(xin)
+    dz = torch.empty_like(xin)
+    x2 = xin.permute(0, 2, 3, 1).reshape(m, c)
+    part = nat.gemm_nt_bn_bwd(a, wt, dz.permute(0, 2, 3, 1).reshape(m, c), dy2, mask, x2, vec)
+    dx, dg, db = nat.bn_bwd_from_partials(dz, xin, vec, bn.weight, True, part)
+    dy = (a.float() @ wt.float().t()).to(torch.bfloat16).view(n, h, w, c).permute(0, 3, 1, 2)
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    rdx, rdg, rdb, rdz = nat.bn_bwd(3, dy, xin, mask, vec, bn.weight, True, dy2, 1)
+    torch.testing.assert_close(dz.float(), rdz.float(), rtol=2e-2, atol=2e-2)
+    for u, v in ((dx, rdx), (dg, rdg), (db, rdb)):
+        torch.testing.assert_close(u.float(), v.float(), rtol=3e-2,
+                                   atol=3e-2 * float(v.float().abs().max()))
+
+
+def test_resnet_bwd_fusion_matches_unfused(cuda, monkeypatch):
+    """A ResNet whose layers have >1 block: conv1's dgrad GEMM runs the previous
+    block's BN backward reduce (gemm_nt_bn_bwd is called) and every parameter
+    gradient is as close to an fp32 eager reference of the same weights as the
+    unfused bf16 path's (bf16 + small-batch BN backward is far from fp32 at random
+    init for BOTH paths, scripts/diag_bwd_fuse.py: ~0.5 relative L2, so the
+    fused path is judged against the unfused path's own error)."""
+    import copy
+
+    from mivod.models.resnet import ResNet, to_mixed_bf16
+    nat = _nat()
+    calls = []
+    real = nat.gemm_nt_bn_bwd
+
+    def counted(*args, **kw):
+        calls.append(args[0].shape)
+        return real(*args, **kw)
+
+    monkeypatch.setattr(nat, "gemm_nt_bn_bwd", counted)
+    torch.manual_seed(0)
+    base = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
+    x = torch.rand(16, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    tgt = torch.randint(0, 10, (16,), device=cuda)
+
+    def grads(m, inp):
+        F.cross_entropy(m(inp).float(), tgt).backward()
+        return {k: p.grad.float() for k, p in m.named_parameters()}
+
+    ref = grads(copy.deepcopy(base).float(), x.float())
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MIVOD_CONV_BN_BWD_FUSE", fuse)
+        out[fuse] = grads(copy.deepcopy(base), x)
+        if fuse == "1":
+            assert len(calls) == 3, calls     # layer1.1, layer2.1, layer3.1
+    for k, r in ref.items():
+        n = float(r.norm()) + 1e-12
+        ef = float((out["1"][k] - r).norm()) / n
+        eu = float((out["0"][k] - r).norm()) / n
+        assert ef <= 1.25 * eu + 2e-3, (k, ef, eu)
