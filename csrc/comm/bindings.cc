@@ -39,13 +39,17 @@ PYBIND11_MODULE(_mvcomm, m) {
 
   py::class_<Comm>(m, "Comm")
       .def(py::init([](py::bytes uid, int rank, int size, int device, double timeout_s,
-                       bool exit_on_abort) {
+                       bool exit_on_abort, int min_ctas, int max_ctas) {
              std::string u = uid;
              py::gil_scoped_release nogil;
-             return std::make_unique<Comm>(u, rank, size, device, timeout_s, exit_on_abort);
+             return std::make_unique<Comm>(u, rank, size, device, timeout_s, exit_on_abort,
+                                           min_ctas, max_ctas);
            }),
            py::arg("uid"), py::arg("rank"), py::arg("size"), py::arg("device"),
-           py::arg("timeout_s") = 0.0, py::arg("exit_on_abort") = false)
+           py::arg("timeout_s") = 0.0, py::arg("exit_on_abort") = false,
+           py::arg("min_ctas") = 0, py::arg("max_ctas") = 0)
+      .def_property_readonly("min_ctas", &Comm::min_ctas)
+      .def_property_readonly("max_ctas", &Comm::max_ctas)
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("size", &Comm::size)
       .def_property_readonly("device", &Comm::device)

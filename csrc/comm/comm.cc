@@ -51,16 +51,25 @@ size_t Comm::dtype_size(int dtype) {
 }
 
 Comm::Comm(const std::string& uid, int rank, int size, int device, double timeout_s,
-           bool exit_on_abort)
-    : rank_(rank), size_(size), device_(device), timeout_s_(timeout_s),
-      exit_on_abort_(exit_on_abort) {
+           bool exit_on_abort, int min_ctas, int max_ctas)
+    : rank_(rank), size_(size), device_(device), min_ctas_(min_ctas), max_ctas_(max_ctas),
+      timeout_s_(timeout_s), exit_on_abort_(exit_on_abort) {
   if (uid.size() != NCCL_UNIQUE_ID_BYTES)
     throw std::invalid_argument("mivod RCCL: unique id must be 128 bytes");
   if (size < 1 || rank < 0 || rank >= size) throw std::invalid_argument("mivod RCCL: bad rank");
   ncclUniqueId id;
   std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
   MV_HIP(hipSetDevice(device));
-  MV_NCCL(ncclCommInitRank(&comm_, size, id, rank));
+  if (min_ctas > 0 || max_ctas > 0) {
+    // CTA (= channel) range of this communicator: how many xGMI rings a collective
+    // spreads over (the RCCL autotune in mivod/parallel/autotune.py sweeps it)
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    if (min_ctas > 0) cfg.minCTAs = min_ctas;
+    if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+    MV_NCCL(ncclCommInitRankConfig(&comm_, size, id, rank, &cfg));
+  } else {
+    MV_NCCL(ncclCommInitRank(&comm_, size, id, rank));
+  }
   start_watchdog();
 }
 
@@ -303,6 +312,8 @@ std::unique_ptr<Comm> Comm::split(int color, int key) {
   c->device_ = device_;
   c->timeout_s_ = timeout_s_;
   c->exit_on_abort_ = exit_on_abort_;
+  c->min_ctas_ = min_ctas_;        // a split child inherits the parent's config
+  c->max_ctas_ = max_ctas_;
   MV_NCCL(ncclCommSplit(comm_, color, key, &c->comm_, nullptr));
   if (c->comm_ == nullptr) return nullptr;     // color == NCCL_SPLIT_NOCOLOR
   MV_NCCL(ncclCommCount(c->comm_, &c->size_));

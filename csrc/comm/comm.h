@@ -43,13 +43,18 @@ struct CommStats {
 class Comm {
  public:
   // Collective: every rank of the communicator calls it with the same arguments.
+  // min_ctas / max_ctas > 0: ncclCommInitRankConfig with that CTA (channel) range
   Comm(const std::string& uid, int rank, int size, int device, double timeout_s,
-       bool exit_on_abort);
+       bool exit_on_abort, int min_ctas = 0, int max_ctas = 0);
   ~Comm();
   Comm(const Comm&) = delete;
   Comm& operator=(const Comm&) = delete;
 
   int rank() const { return rank_; }
+
+  int min_ctas() const { return min_ctas_; }
+
+  int max_ctas() const { return max_ctas_; }
   int size() const { return size_; }
   int device() const { return device_; }
 
@@ -92,6 +97,7 @@ class Comm {
 
   ncclComm_t comm_ = nullptr;
   int rank_ = 0, size_ = 1, device_ = 0;
+  int min_ctas_ = 0, max_ctas_ = 0;
   double timeout_s_ = 0.0;
   bool exit_on_abort_ = false;
 

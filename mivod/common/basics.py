@@ -222,10 +222,25 @@ def _make_gpu_plane(transport: str, world_backend: str, cfg) -> None:
     if transport == "rccl":
         store = dist.distributed_c10d._get_default_store()
         timeout = float(os.environ.get("MIVOD_RCCL_TIMEOUT_S", cfg.stall_shutdown_time_s or 0.0))
-        _state.gpu = RcclTransport.create(
-            _state.rank, _state.size, _state.device, store,
-            key=f"mivod/rccl/{_state.init_count}", timeout_s=timeout,
-            exit_on_abort=cfg.stall_shutdown_time_s > 0)
+        ctas = int(os.environ.get("MIVOD_RCCL_CTAS", "0") or 0)
+
+        def make(c: int, tag: str = "") -> "RcclTransport":
+            return RcclTransport.create(
+                _state.rank, _state.size, _state.device, store,
+                key=f"mivod/rccl/{_state.init_count}{tag}", timeout_s=timeout,
+                exit_on_abort=cfg.stall_shutdown_time_s > 0, min_ctas=c, max_ctas=c)
+
+        if cfg.autotune and ctas == 0 and _state.size > 1:
+            # channel count autotune: one communicator per candidate, keep the fastest
+            from ..parallel.autotune import tune_rccl_ctas
+            mb = 2 ** 20
+            sizes = [cfg.first_bucket_mb * mb, cfg.bucket_mb * mb, cfg.last_bucket_mb * mb]
+            _state.gpu, best, res = tune_rccl_ctas(
+                lambda c: make(c, f"/cta{c}"), lambda t: t.time_allreduce(sizes),
+                log_path=cfg.autotune_log)
+            log.info("RCCL CTA autotune: %s -> %s", res, best or "default")
+        else:
+            _state.gpu = make(ctas)
         _state.backend = "rccl"
         if _hierarchical_topology():
             _state.gpu_local = _state.gpu.split(_state.cross_rank, _state.local_rank)

@@ -9,12 +9,17 @@ U20/U21, §2.6), as used by /root/reference/mnist_keras.py:20,30,87,97 and
 subclass of the optimizer's own class (same class name, so saved models load
 with the plain ``load_model`` as the reference does at mnist_keras.py:124),
 re-instantiated from ``opt.get_config()``, whose ``get_gradients`` averages the
-gradients across ranks when ``size() > 1``.  The averaging is one fused
-collective per dtype: each gradient is submitted to mivod's negotiated engine
-under ``<Name>_Allreduce/<i>`` and the engine packs them into one fusion buffer
-(K1 pack kernel on GPU), reduces once over RCCL (gloo on CPU) and unpacks.
+gradients across ranks when ``size() > 1``.  The averaging runs on a STATIC
+schedule (``_static.StaticGradientReducer``): the plan — one fusion buffer per
+(device, dtype), checked across ranks once — is built on the first step, and
+every step then packs (K1 pack kernel on GPU), reduces once per group over RCCL
+(native TCP ring / gloo on CPU) and unpacks, with no per-step negotiation.
+``MIVOD_KERAS_NEGOTIATED=1`` submits every gradient to the negotiated engine under
+``<Name>_Allreduce/<i>`` instead (horovod's per-tensor protocol).
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -35,11 +40,15 @@ class _DistributedOptimizerMixin:
         self._hvd_compression = compression
         self._hvd_sparse_as_dense = sparse_as_dense
         self._hvd_op = op
+        from ._static import StaticGradientReducer
+        self._hvd_static = StaticGradientReducer(self._hvd_name, op, compression)
 
     def get_gradients(self, loss, params):
         grads = super().get_gradients(loss, params)
         if size() <= 1:
             return grads
+        if os.environ.get("MIVOD_KERAS_NEGOTIATED", "0") != "1":
+            return self._hvd_static(grads)
         handles = []
         for i, g in enumerate(grads):
             if g is None:

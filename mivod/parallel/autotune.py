@@ -16,6 +16,13 @@ candidate runs ``warmup`` + ``trial`` steps and is scored by its median step
 time.  Everything is deterministic, and rank 0's decision is broadcast so all
 ranks re-plan at the same step.  ``HOROVOD_AUTOTUNE_LOG`` gets one CSV row per
 trial.
+
+``tune_rccl_ctas`` is the communicator half: at ``hvd.init()`` (HOROVOD_AUTOTUNE=1,
+mivod RCCL transport, >1 rank) it builds one communicator per candidate CTA count
+(``ncclConfig_t.minCTAs = maxCTAs``: the number of channels, i.e. rings over the 7
+xGMI links, a collective spreads over), times the allreduce of the schedule's
+bucket sizes on each, MAX-reduces the time over ranks (so every rank picks the same
+winner without a broadcast) and keeps the fastest communicator.
 """
 from __future__ import annotations
 
@@ -155,3 +162,36 @@ class BucketAutotuner:
             if new:
                 f.write("first_bucket_mb,bucket_mb,median_step_s,phase,expected_improvement\n")
             f.write(f"{cand[0]:.4g},{cand[1]:.4g},{med:.6f},{phase},{self.last_ei:.4g}\n")
+
+
+# CTA (channel) counts tried by tune_rccl_ctas; 0 = RCCL's own choice
+CTA_CANDIDATES: Tuple[int, ...] = (0, 4, 8, 16, 32)
+
+
+def tune_rccl_ctas(make_comm: Callable[[int], object], time_fn: Callable[[object], float],
+                   candidates=CTA_CANDIDATES, log_path: str = ""):
+    """Pick the CTA count whose communicator runs the bucket allreduces fastest.
+
+    ``make_comm(c)`` builds a communicator with minCTAs = maxCTAs = c (0: default) —
+    collectively, on every rank; ``time_fn(comm)`` returns this schedule's allreduce
+    time in seconds on that communicator, already MAX-reduced over ranks.  Returns
+    (best_comm, best_c, [(c, seconds)]); the other communicators are closed."""
+    results: List[Tuple[int, float]] = []
+    best = None
+    for c in candidates:
+        comm = make_comm(c)
+        t = float(time_fn(comm))
+        results.append((c, t))
+        if log_path:
+            new = not os.path.exists(log_path)
+            with open(log_path, "a") as f:
+                if new:
+                    f.write("rccl_ctas,allreduce_s\n")
+                f.write(f"{c},{t:.6e}\n")
+        if best is None or t < best[2]:
+            if best is not None:
+                best[0].close()
+            best = (comm, c, t)
+        else:
+            comm.close()
+    return best[0], best[1], results

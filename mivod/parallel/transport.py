@@ -63,7 +63,8 @@ class RcclTransport:
 
     @classmethod
     def create(cls, rank: int, size: int, device: torch.device, store=None, key: str = "",
-               timeout_s: float = 0.0, exit_on_abort: bool = False) -> "RcclTransport":
+               timeout_s: float = 0.0, exit_on_abort: bool = False, min_ctas: int = 0,
+               max_ctas: int = 0) -> "RcclTransport":
         m = _mvcomm()
         if size == 1 or store is None:
             uid = m.unique_id()
@@ -73,7 +74,33 @@ class RcclTransport:
         else:
             uid = store.get(key)
         return cls(m.Comm(bytes(uid), rank, size, device.index, float(timeout_s),
-                          bool(exit_on_abort)))
+                          bool(exit_on_abort), int(min_ctas), int(max_ctas)))
+
+    @property
+    def ctas(self):
+        """(minCTAs, maxCTAs) this communicator was created with (0: RCCL default)."""
+        return self.comm.min_ctas, self.comm.max_ctas
+
+    def time_allreduce(self, sizes_bytes, iters: int = 10, warmup: int = 3) -> float:
+        """Seconds for one allreduce of each size in ``sizes_bytes`` (bf16 SUM, the
+        bucket wire), MAX-reduced over ranks — the RCCL autotune objective."""
+        dev = torch.device("cuda", self.comm.device)
+        n = max(int(max(sizes_bytes)) // 2, 1)
+        buf = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        views = [buf[:max(int(b) // 2, 1)] for b in sizes_bytes]
+        for _ in range(warmup):
+            for v in views:
+                self.allreduce_(v)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            for v in views:
+                self.allreduce_(v)
+        e1.record()
+        e1.synchronize()
+        t = torch.tensor([e0.elapsed_time(e1) / 1e3 / iters], dtype=torch.float32, device=dev)
+        self.allreduce_(t, MAX)
+        return float(t.item())
 
     def split(self, color: int, key: int) -> Optional["RcclTransport"]:
         c = self.comm.split(color, key)

@@ -1057,5 +1057,53 @@ def hvd_rank():
     return int(os.environ.get("RANK", "0"))
 
 
+
+def keras_static():
+    """Keras DistributedOptimizer on the static schedule: one plan (checked across
+    ranks) reused every step, same weights as the negotiated per-tensor protocol,
+    identical on every rank; a mismatched gradient set is refused."""
+    import numpy as np
+
+    import mivod.keras as hk
+    import mivod.kerasfw as keras
+    hvd.init()
+    r = hvd.rank()
+    rng = np.random.default_rng(100 + r)
+    xs = rng.standard_normal((6, 16, 8)).astype(np.float32)
+    ys = rng.integers(0, 4, (6, 16)).astype(np.int64)
+
+    def train(negotiated):
+        os.environ["MIVOD_KERAS_NEGOTIATED"] = "1" if negotiated else "0"
+        torch.manual_seed(0)
+        model = keras.Sequential([keras.layers.Dense(16, activation="relu"),
+                                  keras.layers.Dense(4)])
+        opt = hk.DistributedOptimizer(keras.optimizers.SGD(0.1, momentum=0.9))
+        model.compile(loss=keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=opt)
+        for x, y in zip(xs, ys):
+            model.train_on_batch(x, y)
+        flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+        return flat, opt
+
+    fs, opt_s = train(False)
+    fn, _ = train(True)
+    assert opt_s._hvd_static.plans == 1, opt_s._hvd_static.plans
+    torch.testing.assert_close(fs, fn, rtol=1e-5, atol=1e-6)
+    allf = hvd.allgather(fs.unsqueeze(0))
+    assert torch.equal(allf[0], allf[1])
+    # a rank-dependent gradient list must be refused by the plan check
+    from mivod.keras._static import StaticGradientReducer
+    red = StaticGradientReducer("Bad", hk.Average, hk.Compression.none)
+    gs = [torch.ones(3 + r)]
+    try:
+        red(gs)
+    except RuntimeError as e:
+        assert "differ across ranks" in str(e)
+    else:
+        raise AssertionError("mismatched plans were not detected")
+    hvd.shutdown()
+    print("OK", r)
+
+
 if __name__ == "__main__":
     globals()[sys.argv[1]]()

@@ -92,6 +92,11 @@ def test_keras_tf2_style_2ranks():
     assert "finished gradual learning rate warmup" in outs[0]
 
 
+def test_keras_static_schedule_2ranks():
+    """Keras gradients on the static schedule == the negotiated protocol."""
+    run_ranks("keras_static", 2, timeout=300)
+
+
 def test_hierarchical_allreduce_2x2():
     run_ranks("hierarchical", 4, local_size=2)
 

@@ -36,3 +36,28 @@ def test_gpu_xgmi_mesh_one_shot_allreduce(cuda):
     """K7: the HIP-IPC mesh allreduce kernel between two processes on one GPU."""
     run_ranks("gpu_mesh", 2, timeout=180,
               extra_env={"MIVOD_TRANSPORT": "gloo-gpu", "MIVOD_MESH_MAX_MB": "1"})
+
+
+def test_gpu_rccl_cta_config_and_autotune(cuda):
+    """ncclCommInitRankConfig with a CTA range, and the CTA autotune loop over real
+    communicators (world 1: the sweep mechanics, not the timing, are what is tested)."""
+    import torch
+
+    from mivod.parallel.autotune import tune_rccl_ctas
+    from mivod.parallel.transport import RcclTransport
+    made = []
+
+    def make(c):
+        t = RcclTransport.create(0, 1, cuda, min_ctas=c, max_ctas=c)
+        made.append(t)
+        return t
+
+    best, c, res = tune_rccl_ctas(make, lambda t: t.time_allreduce([2 ** 20, 4 * 2 ** 20], iters=2),
+                                  candidates=(0, 4, 8))
+    assert [r[0] for r in res] == [0, 4, 8] and all(r[1] >= 0 for r in res)
+    assert best.ctas == (c, c)
+    x = torch.arange(1000, dtype=torch.float32, device=cuda)
+    best.allreduce_(x)
+    torch.cuda.synchronize()
+    assert torch.equal(x, torch.arange(1000, dtype=torch.float32, device=cuda))
+    best.close()

@@ -198,3 +198,31 @@ def test_fault_kinds_end_the_job(kind, step):
         assert "timed out" in r.stderr or "stall" in r.stderr.lower(), r.stderr[-3000:]
     else:
         assert "injected fault" in r.stderr
+
+
+def test_rccl_cta_autotune_picks_fastest_and_closes_the_rest(tmp_path):
+    """tune_rccl_ctas: one communicator per candidate, the (rank-MAX) fastest kept,
+    every other closed, one CSV row per candidate."""
+    from mivod.parallel.autotune import tune_rccl_ctas
+
+    class FakeComm:
+        def __init__(self, c):
+            self.c, self.closed = c, False
+
+        def close(self):
+            self.closed = True
+
+    times = {0: 3.0, 4: 2.5, 8: 1.0, 16: 1.5, 32: 1.0}
+    made = []
+
+    def make(c):
+        made.append(FakeComm(c))
+        return made[-1]
+
+    log = tmp_path / "at.csv"
+    best, c, res = tune_rccl_ctas(make, lambda comm: times[comm.c], log_path=str(log))
+    assert c == 8 and best.c == 8 and not best.closed      # first of the tied minimum
+    assert [m.closed for m in made] == [True, True, False, True, True]
+    assert res == [(0, 3.0), (4, 2.5), (8, 1.0), (16, 1.5), (32, 1.0)]
+    rows = log.read_text().splitlines()
+    assert rows[0] == "rccl_ctas,allreduce_s" and len(rows) == 6
