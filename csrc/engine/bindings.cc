@@ -3,6 +3,7 @@
 #include <pybind11/stl.h>
 
 #include "controller.h"
+#include "loop.h"
 #include "ring.h"
 #include "timeline.h"
 
@@ -107,7 +108,7 @@ PYBIND11_MODULE(_mvcore, m) {
       .def_readwrite("connect_timeout_s", &ControllerConfig::connect_timeout_s)
       .def_readwrite("cache_capacity", &ControllerConfig::cache_capacity);
 
-  py::class_<Controller>(m, "Controller")
+  py::class_<Controller, std::shared_ptr<Controller>>(m, "Controller")
       .def(py::init<const ControllerConfig&>())
       .def("listen", &Controller::listen, py::call_guard<py::gil_scoped_release>())
       .def("connect", &Controller::connect, py::call_guard<py::gil_scoped_release>())
@@ -149,4 +150,36 @@ PYBIND11_MODULE(_mvcore, m) {
       .def_property_readonly("bitvector_cycles", &Controller::bitvector_cycles)
       .def_property_readonly("cache_size", &Controller::cache_size)
       .def("close", &Controller::close, py::call_guard<py::gil_scoped_release>());
+
+  // background negotiation loop (native thread; Python executes the responses)
+  py::class_<EngineLoop>(m, "EngineLoop")
+      .def(py::init<std::shared_ptr<Controller>, int, double>(), py::arg("controller"),
+           py::arg("size"), py::arg("cycle_s"))
+      .def("submit",
+           [](EngineLoop& l, py::list reqs) {
+             std::vector<Request> rs;
+             rs.reserve(reqs.size());
+             for (auto h : reqs) rs.push_back(to_request(h));
+             py::gil_scoped_release nogil;
+             l.submit(std::move(rs));
+           })
+      .def("set_position", &EngineLoop::set_position)
+      .def("request_shutdown", &EngineLoop::request_shutdown,
+           py::call_guard<py::gil_scoped_release>())
+      .def("wait",
+           [](EngineLoop& l, double timeout_s) -> py::object {
+             CycleResult r;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = l.wait(timeout_s, &r);
+             }
+             if (!ok) return py::none();
+             return py::make_tuple(to_py(r.responses), r.all_shutdown, r.exec_at, r.error);
+           },
+           py::arg("timeout_s") = -1.0)
+      .def("join", &EngineLoop::join, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("finished", &EngineLoop::finished)
+      .def_property_readonly("cycles", &EngineLoop::cycles)
+      .def_property_readonly("requests", &EngineLoop::requests);
 }

@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import itertools
 import logging
+import os
 import threading
 import time
 from typing import Dict, List, Optional
@@ -141,6 +142,8 @@ class Engine:
         self.stream = None
         self.fusion: Dict[tuple, torch.Tensor] = {}
         self.controller = None
+        self.loop = None
+        self.native = False
         self.tl = None
 
     # ------------------------------------------------------------ lifecycle
@@ -151,13 +154,27 @@ class Engine:
             self.stream = st.comm_stream or torch.cuda.Stream(device=st.device, priority=-1)
         from ..utils import timeline as TL
         self.tl = TL.get()
-        if st.size == 1:
-            self.controller = LocalController(self.cfg.fusion_threshold)
-        else:
+        self.native = os.environ.get("MIVOD_ENGINE", "native") != "python"
+        if self.native:
+            # negotiation cycle in a native thread (csrc/engine/loop.cc); this
+            # process's Python only enqueues and executes responses
             from .controller import make_controller
+            from .. import _mvcore  # type: ignore
             self.controller = make_controller(st, self.cfg)
+            cycle = max(self.cfg.cycle_time_ms, 0.0) / 1000.0
+            self.loop = _mvcore.EngineLoop(self.controller.ctl, st.size, cycle)
+            ORDER.on_position = self.loop.set_position
+            self.loop.set_position(ORDER.position())
+            target = self._exec_loop
+        else:
+            if st.size == 1:
+                self.controller = LocalController(self.cfg.fusion_threshold)
+            else:
+                from .controller import make_controller
+                self.controller = make_controller(st, self.cfg)
+            target = self._loop
         self.running = True
-        self.thread = threading.Thread(target=self._loop, name="mivod-engine", daemon=True)
+        self.thread = threading.Thread(target=target, name="mivod-engine", daemon=True)
         self.thread.start()
 
     def stop(self):
@@ -166,8 +183,15 @@ class Engine:
         with self.cv:
             self.running = False
             self.cv.notify_all()
+        if self.loop is not None:
+            self.loop.request_shutdown()
         if self.thread is not None:
             self.thread.join(timeout=30)
+        if self.loop is not None:
+            if ORDER.on_position == self.loop.set_position:
+                ORDER.on_position = None
+            if self.loop.finished:
+                self.loop.join()
         if self.controller is not None:
             self.controller.close()
 
@@ -189,13 +213,56 @@ class Engine:
             self.inflight[name] = h
             if tensor.is_cuda:
                 ORDER.submitted(1)      # direct GPU collectives wait for its response
-            self.pending.append(h)
-            self.cv.notify_all()
+            if self.loop is None:
+                self.pending.append(h)
+                self.cv.notify_all()
         if self.tl is not None:
             self.tl.start(name, "QUEUE")
+        if self.loop is not None:
+            self.loop.submit([h.request(self.st.device.index if tensor.is_cuda else -1)])
         return h
 
     # ----------------------------------------------------------------- loop
+    def _exec_loop(self):
+        """Executor of the native loop's responses (GIL released while waiting)."""
+        while True:
+            r = self.loop.wait(1.0)
+            if r is None:
+                if self.loop.finished:
+                    break
+                continue
+            responses, all_shutdown, exec_at, err = r
+            if err:
+                log.error("mivod negotiation failed: %s", err)
+                self._fail_all(HorovodInternalError(err))
+                break
+            with self.cv:
+                waiting = dict(self.inflight)
+            self._dispatch(responses, exec_at, waiting)
+            if all_shutdown:
+                self._fail_all(HorovodInternalError("mivod shut down with pending operations"))
+                break
+
+    def _dispatch(self, responses, exec_at, waiting):
+        gpu_fns, n_gpu = [], 0
+        for kind, names, err in responses:
+            hs = [waiting.pop(n) for n in names if n in waiting]
+            if not hs:
+                continue
+            on_gpu = hs[0].tensor.is_cuda
+            if on_gpu:
+                n_gpu += len(hs)
+            if err:
+                for h in hs:
+                    self._finish(h, error=HorovodInternalError(err))
+                continue
+            if on_gpu:
+                gpu_fns.append(lambda kind=kind, hs=hs: self._run(kind, hs))
+            else:
+                self._run(kind, hs)
+        if n_gpu:
+            ORDER.responded(exec_at, n_gpu, gpu_fns)
+
     def _loop(self):
         cycle = max(self.cfg.cycle_time_ms, 0.0) / 1000.0
         self._waiting: Dict[str, Handle] = {}
@@ -216,24 +283,7 @@ class Engine:
                 log.error("mivod negotiation failed: %s", e)
                 self._fail_all(HorovodInternalError(str(e)))
                 break
-            gpu_fns, n_gpu = [], 0
-            for kind, names, err in responses:
-                hs = [self._waiting.pop(n) for n in names if n in self._waiting]
-                if not hs:
-                    continue
-                on_gpu = hs[0].tensor.is_cuda
-                if on_gpu:
-                    n_gpu += len(hs)
-                if err:
-                    for h in hs:
-                        self._finish(h, error=HorovodInternalError(err))
-                    continue
-                if on_gpu:
-                    gpu_fns.append(lambda kind=kind, hs=hs: self._run(kind, hs))
-                else:
-                    self._run(kind, hs)
-            if n_gpu:
-                ORDER.responded(exec_at, n_gpu, gpu_fns)
+            self._dispatch(responses, exec_at, self._waiting)
             if stopping and all_shutdown:
                 self._fail_all(HorovodInternalError("mivod shut down with pending operations"))
                 break
@@ -249,6 +299,9 @@ class Engine:
 
     def _fail_all(self, err):
         n_gpu = 0
+        if self.loop is not None:
+            with self.cv:
+                self._waiting = dict(self.inflight)
         for h in list(self._waiting.values()):
             n_gpu += int(h.tensor.is_cuda)
             self._finish(h, error=err)

@@ -30,6 +30,8 @@ class NativeController:
         tl = TL.get()
         if tl is not None and isinstance(tl, _mvcore.Timeline):
             self.ctl.set_timeline(tl)
+        if state.size == 1:
+            return                      # 1-rank world: coordinate() locally, no sockets
         store = dist.distributed_c10d._get_default_store()
         key = "mivod/controller"
         if state.rank == 0:

@@ -48,6 +48,9 @@ class IssueOrder:
         self._draining = False
         self.enabled = False       # multi-rank GPU world only
         self.waits = 0             # direct issues that had to wait for a response (stats)
+        # called with the new Q after every issue (the native engine loop reports
+        # it to the coordinator each cycle without taking this lock)
+        self.on_position = None
 
     def reset(self, enabled: bool):
         with self.cv:
@@ -56,6 +59,8 @@ class IssueOrder:
             self.deferred = []
             self.enabled = enabled
             self.waits = 0
+            if self.on_position is not None:
+                self.on_position(0)
 
     # -------------------------------------------------------------- direct
     @contextlib.contextmanager
@@ -72,6 +77,8 @@ class IssueOrder:
                     self.cv.wait()
             yield
             self.q += 1
+            if self.on_position is not None:
+                self.on_position(self.q)
             self._drain()
 
     # --------------------------------------------------------------- named

@@ -57,6 +57,11 @@ def test_basics_4ranks():
     run_ranks("basics", 4)
 
 
+def test_basics_2ranks_python_engine_loop():
+    """The Python fallback of the negotiation loop (MIVOD_ENGINE=python) still works."""
+    run_ranks("basics", 2, extra_env={"MIVOD_ENGINE": "python"})
+
+
 def test_negotiation_errors():
     run_ranks("errors", 2)
 
