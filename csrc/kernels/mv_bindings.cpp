@@ -14,6 +14,7 @@
 #include "mv_bert.h"
 #include "mv_bn.h"
 #include "mv_gemm.h"
+#include "mv_conv.h"
 #include "mv_kernels.h"
 #include "mv_pool.h"
 
@@ -906,6 +907,53 @@ std::vector<at::Tensor> bn_bwd_from_partials(at::Tensor dz, at::Tensor x, at::Te
   return {dx, dg, db};
 }
 
+// ---------------------------------------------------------------------------
+// implicit-GEMM 3x3 convolution (pad 1), channels_last bf16
+// ---------------------------------------------------------------------------
+int64_t conv3x3_partials(int64_t M, int64_t K) { return mv_conv3x3_partials(M, (int)K); }
+
+// y = conv3x3(x, w, stride, pad 1) (+ BN statistics partials of y around shift)
+at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> shift,
+                   c10::optional<at::Tensor> partial) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3: x must be a channels_last bf16 GPU tensor [N, C, H, W]");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 &&
+                  w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3: w must be a channels_last bf16 [K, C, 3, 3] filter matching x");
+  TORCH_CHECK(w.device() == x.device(), "conv3x3: devices differ");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = w.size(0);
+  TORCH_CHECK(C % 64 == 0 && K % 64 == 0 && C > 0 && K > 0, "conv3x3: C and K must be multiples of 64");
+  TORCH_CHECK(stride == 1 || stride == 2, "conv3x3: stride must be 1 or 2");
+  TORCH_CHECK(N * H * W * std::max(C, K) < (int64_t(1) << 40) && H < 65536 && W < 65536,
+              "conv3x3: too large");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const int64_t M = N * Ho * Wo;
+  TORCH_CHECK(M > 0, "conv3x3: empty input");
+  c10::DeviceGuard guard(x.device());
+  at::Tensor y = at::empty({N, K, Ho, Wo}, x.options(), at::MemoryFormat::ChannelsLast);
+  float* pp = nullptr;
+  const float* sp = nullptr;
+  if (partial.has_value() && partial->defined()) {
+    TORCH_CHECK(partial->is_cuda() && partial->scalar_type() == at::kFloat &&
+                    partial->is_contiguous() && partial->numel() >= conv3x3_partials(M, K) * 2 * K &&
+                    partial->device() == x.device(),
+                "conv3x3: partial must be fp32 [P, 2, K] with P = conv3x3_partials(M, K)");
+    pp = partial->data_ptr<float>();
+    if (shift.has_value() && shift->defined()) {
+      TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->numel() == K &&
+                      shift->is_contiguous(),
+                  "conv3x3: shift must be fp32 [K]");
+      sp = shift->data_ptr<float>();
+    }
+  }
+  TORCH_CHECK(mv_conv3x3(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)C,
+                         (int)K, (int)stride, sp, pp, cur_stream()),
+              "conv3x3: unsupported shape");
+  return y;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -956,5 +1004,9 @@ PYBIND11_MODULE(_mvk, m) {
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bn") = 0);
   m.def("bn_bwd_from_partials", &bn_bwd_from_partials,
         "BN backward finalize + dx from GEMM-epilogue partials -> (dx, dgamma, dbeta)");
+  m.def("conv3x3", &conv3x3, "implicit-GEMM 3x3 conv (pad 1) with optional fused BN statistics",
+        py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("shift") = py::none(),
+        py::arg("partial") = py::none());
+  m.def("conv3x3_partials", &conv3x3_partials, "partial rows of conv3x3's statistics epilogue");
   m.def("gemm_partials", &gemm_partials, "row tiles (statistics partial rows) of gemm_nt");
 }

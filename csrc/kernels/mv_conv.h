@@ -1,0 +1,13 @@
+// Implicit-GEMM 3x3 convolution (pad 1, stride 1/2), NHWC bf16, gfx950 MFMA (mv_conv.hip)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+// partial rows [P][2][K] of the fused BN-statistics epilogue for an M-pixel output
+int64_t mv_conv3x3_partials(int64_t M, int K);
+// y[N, Ho, Wo, K] = conv3x3(x[N, H, W, C], w[K, 3, 3, C]); C, K multiples of 64.
+// partial != null: BN statistics of the bf16 outputs around shift (may be null = 0).
+// Returns false for an unsupported shape (nothing launched).
+bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int C, int K,
+                int stride, const float* shift, float* partial, hipStream_t st);

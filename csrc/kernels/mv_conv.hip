@@ -1,0 +1,316 @@
+// Implicit-GEMM 3x3 convolution (pad 1, stride 1 or 2) on gfx950 MFMA, NHWC bf16.
+//
+//   Y[m, k] = sum_{r, s, c} X[n, ho*st - 1 + r, wo*st - 1 + s, c] . W[k, r, s, c]
+//   m = (n, ho, wo) — a GEMM with M = N*Ho*Wo, N = Cout, K = 9*Cin whose A operand
+//   (im2col(X)) is never materialised: every 64-channel K step of the tile reads one
+//   filter tap's rows of X straight into LDS.
+//
+// Staging: global_load_lds (16 bytes per lane, no VGPR round trip) into a
+// double-buffered LDS image; the next K step's loads — including the first step of
+// the workgroup's NEXT output tile — are in flight while the current step runs on
+// the matrix cores.  The LDS image is lane-linear (the LDS-DMA writes base + lane*16),
+// so the 16-byte-chunk XOR swizzle that keeps the fragment reads conflict-free is
+// applied to the per-lane GLOBAL source address (slot (row, c) holds chunk
+// c ^ (row & 7)) and undone on the read.  Padding taps read a zero page.
+//
+// Persistent tiles: a workgroup owns one column tile (BN output channels) and walks
+// output-row tiles mt = stream, stream + nstreams, ...; with STATS the following
+// BatchNorm's per-channel sums (of the bf16-rounded outputs around shift) accumulate
+// in registers over all of them and one [2][BN] partial row per stream is written —
+// the layout of the BN finalize (mv_bn.hip), as in mv_gemm.hip.
+//
+// MFMA mapping as mv_gemm.hip: the filter tile is the A operand, so each lane's 4
+// accumulators are 4 consecutive output channels of one output pixel (8-byte stores).
+#include "mv_common.h"
+#include "mv_conv.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace mv {
+namespace conv {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int BM = 128;             // output pixels per tile
+constexpr int BK = 64;              // input channels per K step (one tap)
+constexpr int NT = 256;             // 4 waves, 2 x 2
+constexpr int A_CH = BM * 8 / NT;   // 16-byte chunks per thread per A stage
+
+__device__ __attribute__((aligned(16))) uint32_t g_zero[32];   // zero page for padding taps
+
+__device__ __forceinline__ f32x4v mfma(const bf16x8& a, const bf16x8& b, const f32x4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ (row & 7)) << 3); }
+__device__ __forceinline__ float round_bf16(float x) { return (float)(__bf16)x; }
+
+__device__ __forceinline__ int remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ void glds16(const void* src, __bf16* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0,
+                                   0);
+}
+
+struct Geo {
+  int H, W, C, Ho, Wo, K, st;
+  int64_t M;
+};
+
+// per-thread state of the A rows it stages (4 rows, fixed source chunk)
+struct RowInfo {
+  int64_t base[A_CH];   // element offset of (n, hi0, wi0, 0) — may be "negative"
+  int hi0[A_CH], wi0[A_CH];
+};
+
+__device__ __forceinline__ void row_info(const Geo& g, int64_t m0, int tid, RowInfo& ri) {
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int64_t m = m0 + i * (NT / 8) + (tid >> 3);
+    if (m < g.M) {
+      const int64_t hw = (int64_t)g.Ho * g.Wo;
+      const int n = (int)(m / hw);
+      const int rem = (int)(m - (int64_t)n * hw);
+      const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
+      ri.hi0[i] = ho * g.st - 1;
+      ri.wi0[i] = wo * g.st - 1;
+      ri.base[i] = (((int64_t)n * g.H + ri.hi0[i]) * g.W + ri.wi0[i]) * g.C;
+    } else {
+      ri.hi0[i] = -1000000;     // every tap out of bounds -> zero rows
+      ri.wi0[i] = -1000000;
+      ri.base[i] = 0;
+    }
+  }
+}
+
+template <int BN, bool STATS>
+__global__ __launch_bounds__(NT) void conv3x3_kernel(
+    const __bf16* __restrict__ X, const __bf16* __restrict__ Wt, __bf16* __restrict__ Y, Geo g,
+    int ntn, int64_t ntm, const float* __restrict__ shift, float* __restrict__ partial) {
+  constexpr int WTN = BN / 2, WTM = BM / 2;
+  constexpr int TN = WTN / 16, TM = WTM / 16;
+  constexpr int B_CH = BN * 8 / NT;
+  constexpr int STAGE = (BM + BN) * BK;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int t = remap(blockIdx.x, gridDim.x);
+  const int nt = t % ntn;
+  const int64_t stream = t / ntn, nstreams = gridDim.x / ntn;
+  const int n0 = nt * BN;
+  const int csteps = g.C / BK, KT = 9 * csteps;
+  const int64_t wrow = (int64_t)9 * g.C;          // filter row length
+  const int sc = (tid & 7) ^ ((tid >> 3) & 7);    // swizzled source chunk of this thread
+
+  auto issue = [&](const RowInfo& ri, int kt, int buf) {
+    const int tap = kt / csteps, c0 = (kt - tap * csteps) * BK;
+    const int r = tap / 3, s = tap - r * 3;
+    __bf16* As = smem + buf * STAGE;
+    __bf16* Bs = As + BM * BK;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int hi = ri.hi0[i] + r, wi = ri.wi0[i] + s;
+      const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+      const void* src = ok ? (const void*)(X + ri.base[i] + ((int64_t)r * g.W + s) * g.C + c0 + sc * 8)
+                           : (const void*)(g_zero + (tid & 7) * 4);
+      glds16(src, As + (i * NT + wid * 64) * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = i * (NT / 8) + (tid >> 3);
+      glds16(Wt + (int64_t)(n0 + row) * wrow + tap * g.C + c0 + sc * 8, Bs + (i * NT + wid * 64) * 8);
+    }
+  };
+
+  const int gq = lane >> 4, rl = lane & 15;
+  float sh[TN][4], s1[TN][4], s2[TN][4];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = n0 + wn * WTN + a * 16 + 4 * gq + r;
+      sh[a][r] = (STATS && shift) ? shift[col] : 0.f;
+      s1[a][r] = 0.f;
+      s2[a][r] = 0.f;
+    }
+  f32x4v acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  int64_t mt = stream;
+  if (mt < ntm) {
+    RowInfo cur, nxt;
+    row_info(g, mt * BM, tid, cur);
+    issue(cur, 0, 0);
+    __syncthreads();
+    int kt = 0, buf = 0;
+    while (true) {
+      int kt2 = kt + 1;
+      int64_t mt2 = mt;
+      if (kt2 == KT) {
+        kt2 = 0;
+        mt2 += nstreams;
+        if (mt2 < ntm) row_info(g, mt2 * BM, tid, nxt);
+      }
+      const bool more = mt2 < ntm;
+      if (more) issue(kt2 == 0 ? nxt : cur, kt2, buf ^ 1);
+      const __bf16* As = smem + buf * STAGE;
+      const __bf16* Bs = As + BM * BK;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        const int ch = kk * 4 + gq;
+        bf16x8 wf[TN], af[TM];
+#pragma unroll
+        for (int a = 0; a < TN; ++a)
+          wf[a] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WTN + a * 16 + rl, ch));
+#pragma unroll
+        for (int b = 0; b < TM; ++b)
+          af[b] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WTM + b * 16 + rl, ch));
+#pragma unroll
+        for (int a = 0; a < TN; ++a)
+#pragma unroll
+          for (int b = 0; b < TM; ++b) acc[a][b] = mfma(wf[a], af[b], acc[a][b]);
+      }
+      if (kt == KT - 1) {      // tile done: store (+ statistics) while the next loads fly
+        const int64_t m0 = mt * BM;
+#pragma unroll
+        for (int b = 0; b < TM; ++b) {
+          const int64_t row = m0 + wm * WTM + b * 16 + rl;
+          if (row < g.M) {
+#pragma unroll
+            for (int a = 0; a < TN; ++a) {
+              const f32x4v v = acc[a][b];
+              const int col = n0 + wn * WTN + a * 16 + 4 * gq;
+              *reinterpret_cast<u32x2*>(Y + row * g.K + col) =
+                  u32x2{cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3])};
+              if (STATS) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const float d = round_bf16(v[r]) - sh[a][r];
+                  s1[a][r] += d;
+                  s2[a][r] += d * d;
+                }
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < TN; ++a)
+#pragma unroll
+          for (int b = 0; b < TM; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      }
+      __syncthreads();         // next stage landed (vmcnt drained) and this one is consumed
+      if (!more) break;
+      if (kt2 == 0) cur = nxt;
+      kt = kt2;
+      mt = mt2;
+      buf ^= 1;
+    }
+  }
+  if (!STATS) return;
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[a][r] += __shfl_xor(s1[a][r], o, kWave);
+        s2[a][r] += __shfl_xor(s2[a][r], o, kWave);
+      }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);      // [2][2 (wm)][BN]
+  if (rl == 0) {
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = wn * WTN + a * 16 + 4 * gq + r;
+        red[(0 * 2 + wm) * BN + c] = s1[a][r];
+        red[(1 * 2 + wm) * BN + c] = s2[a][r];
+      }
+  }
+  __syncthreads();
+  if (stream >= ntm) return;
+  for (int v = tid; v < 2 * BN; v += NT) {
+    const int k = v / BN, c = v - k * BN;
+    partial[(stream * 2 + k) * g.K + n0 + c] = red[(k * 2 + 0) * BN + c] + red[(k * 2 + 1) * BN + c];
+  }
+}
+
+template <int BN, bool STATS>
+static int64_t streams_for(int64_t ntm, int ntn) {
+  static int per = [] {
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, (const void*)&conv3x3_kernel<BN, STATS>,
+                                                     NT, 0) != hipSuccess || v < 1)
+      v = 1;
+    return v;
+  }();
+  static int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  int64_t s = (int64_t)cus * per / ntn;
+  const char* e = std::getenv("MIVOD_CONV_WAVES");   // tiles in flight per CU (A/B knob)
+  if (e && std::atoi(e) > 0) s = (int64_t)cus * std::atoi(e) / ntn;
+  s = std::max<int64_t>(1, std::min(s, ntm));
+  return s;
+}
+
+}  // namespace conv
+}  // namespace mv
+
+static int conv_bn_of(int K) { return K % 128 == 0 ? 128 : 64; }
+
+int64_t mv_conv3x3_partials(int64_t M, int K) {
+  using namespace mv::conv;
+  const int bn = conv_bn_of(K);
+  const int64_t ntm = (M + BM - 1) / BM;
+  return bn == 128 ? streams_for<128, true>(ntm, K / 128) : streams_for<64, true>(ntm, K / 64);
+}
+
+bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int C, int K,
+                int stride, const float* shift, float* partial, hipStream_t st) {
+  using namespace mv::conv;
+  if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2)) return false;
+  Geo g;
+  g.H = H;
+  g.W = W;
+  g.C = C;
+  g.K = K;
+  g.st = stride;
+  g.Ho = (H - 1) / stride + 1;
+  g.Wo = (W - 1) / stride + 1;
+  g.M = (int64_t)N * g.Ho * g.Wo;
+  const int64_t ntm = (g.M + BM - 1) / BM;
+  const __bf16* X = (const __bf16*)x;
+  const __bf16* Wt = (const __bf16*)w;
+  __bf16* Y = (__bf16*)y;
+#define MV_LAUNCH(BNV, ST)                                                                      \
+  {                                                                                             \
+    const int ntn = K / BNV;                                                                    \
+    const int64_t ns = streams_for<BNV, ST>(ntm, ntn);                                          \
+    hipLaunchKernelGGL((conv3x3_kernel<BNV, ST>), dim3((unsigned)(ns * ntn)), dim3(NT), 0, st, X, \
+                       Wt, Y, g, ntn, ntm, shift, partial);                                     \
+  }
+  if (conv_bn_of(K) == 128) {
+    if (partial) MV_LAUNCH(128, true) else MV_LAUNCH(128, false)
+  } else {
+    if (partial) MV_LAUNCH(64, true) else MV_LAUNCH(64, false)
+  }
+#undef MV_LAUNCH
+  return true;
+}

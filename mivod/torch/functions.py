@@ -82,8 +82,8 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
         for _name, p in items:
             if torch.is_tensor(p):
                 torch.autograd.graph.increment_version(p)
-    if tensors and tensors[0].is_cuda:
-        torch.cuda.current_stream().synchronize()
+    # no host synchronisation: pack, broadcast and unpack are all enqueued on the
+    # caller's current stream (transport.py), so later work on it is ordered after them
 
 
 def broadcast_optimizer_state(optimizer, root_rank: int = 0) -> None:
@@ -184,8 +184,7 @@ def broadcast_optimizer_state(optimizer, root_rank: int = 0) -> None:
             a.versions = [p._version for p in a.params]
     else:
         optimizer.load_state_dict(state_dict)
-    if tensors and tensors[0].is_cuda:
-        torch.cuda.current_stream().synchronize()
+    # stream-ordered like broadcast_parameters: no host synchronisation
 
 
 def broadcast_object(obj, root_rank: int = 0, name=None):

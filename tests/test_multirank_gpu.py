@@ -61,3 +61,27 @@ def test_gpu_rccl_cta_config_and_autotune(cuda):
     torch.cuda.synchronize()
     assert torch.equal(x, torch.arange(1000, dtype=torch.float32, device=cuda))
     best.close()
+
+
+# ---- real multi-GPU RCCL (skipped on a 1-GPU box: RCCL refuses 2 ranks per device)
+def _gpus():
+    import torch
+    return torch.cuda.device_count()
+
+
+_MULTI = pytest.mark.skipif(_gpus() < 2, reason="needs >= 2 GPUs")
+
+
+@_MULTI
+@pytest.mark.parametrize("scenario", ["gpu_dist", "gpu_adasum", "gpu_order"])
+def test_rccl_two_gpus(cuda, scenario):
+    """The hook path, fp16-wire Adasum and the one-issue-order protocol over mivod's
+    own RCCL communicator, one rank per GPU."""
+    run_ranks(scenario, 2, timeout=240, extra_env={"MIVOD_TRANSPORT": "rccl"})
+
+
+@_MULTI
+def test_xgmi_mesh_two_gpus(cuda):
+    """K7 one-shot allreduce between two GPUs' IPC-mapped staging buffers."""
+    run_ranks("gpu_mesh", 2, timeout=240,
+              extra_env={"MIVOD_TRANSPORT": "rccl", "MIVOD_MESH_MAX_MB": "1"})
