@@ -5,10 +5,10 @@
 //   (im2col(X)) is never materialised: every 64-channel K step of the tile reads one
 //   filter tap's rows of X straight into LDS.
 //
-// Staging: global_load_lds (16 bytes per lane, no VGPR round trip) into a
-// double-buffered LDS image; the next K step's loads — including the first step of
-// the workgroup's NEXT output tile — are in flight while the current step runs on
-// the matrix cores.  The LDS image is lane-linear (the LDS-DMA writes base + lane*16),
+// Staging: global_load_lds (16 bytes per lane, no VGPR round trip) into a 3-slot
+// LDS ring; the loads of the next TWO K steps — across the boundary into the
+// workgroup's next output tile — are in flight while the current step runs on the
+// matrix cores (counted vmcnt waits + raw s_barrier, so they survive the barrier).  The LDS image is lane-linear (the LDS-DMA writes base + lane*16),
 // so the 16-byte-chunk XOR swizzle that keeps the fragment reads conflict-free is
 // applied to the per-lane GLOBAL source address (slot (row, c) holds chunk
 // c ^ (row & 7)) and undone on the read.  Padding taps read a zero page.
@@ -34,10 +34,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int BM = 128;             // output pixels per tile
 constexpr int BK = 64;              // input channels per K step (one tap)
-constexpr int NT = 256;             // 4 waves, 2 x 2
-constexpr int A_CH = BM * 8 / NT;   // 16-byte chunks per thread per A stage
+constexpr int NT = 256;             // 4 waves
 
 __device__ __attribute__((aligned(16))) uint32_t g_zero[32];   // zero page for padding taps
 
@@ -64,44 +62,71 @@ struct Geo {
   int64_t M;
 };
 
-// per-thread state of the A rows it stages (4 rows, fixed source chunk)
+// per-thread state of the A rows it stages (A_CH rows, fixed source chunk): the byte
+// address of tap (0, 0) and a 9-bit mask of the taps that fall inside the image —
+// per K step only a wave-uniform offset is added (keeps the issue path a few VALU ops)
+template <int A_CH>
 struct RowInfo {
-  int64_t base[A_CH];   // element offset of (n, hi0, wi0, 0) — may be "negative"
-  int hi0[A_CH], wi0[A_CH];
+  uint64_t addr[A_CH];
+  uint32_t valid[A_CH];
 };
 
-__device__ __forceinline__ void row_info(const Geo& g, int64_t m0, int tid, RowInfo& ri) {
+template <int A_CH>
+__device__ __forceinline__ void row_info(const Geo& g, const __bf16* X, int64_t m0, int tid,
+                                         int sc, RowInfo<A_CH>& ri) {
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
     const int64_t m = m0 + i * (NT / 8) + (tid >> 3);
+    ri.valid[i] = 0;
+    ri.addr[i] = 0;
     if (m < g.M) {
       const int64_t hw = (int64_t)g.Ho * g.Wo;
       const int n = (int)(m / hw);
       const int rem = (int)(m - (int64_t)n * hw);
       const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
-      ri.hi0[i] = ho * g.st - 1;
-      ri.wi0[i] = wo * g.st - 1;
-      ri.base[i] = (((int64_t)n * g.H + ri.hi0[i]) * g.W + ri.wi0[i]) * g.C;
-    } else {
-      ri.hi0[i] = -1000000;     // every tap out of bounds -> zero rows
-      ri.wi0[i] = -1000000;
-      ri.base[i] = 0;
+      const int hi0 = ho * g.st - 1, wi0 = wo * g.st - 1;
+      uint32_t v = 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const bool ok = (unsigned)(hi0 + r) < (unsigned)g.H && (unsigned)(wi0 + s) < (unsigned)g.W;
+          v |= (ok ? 1u : 0u) << (r * 3 + s);
+        }
+      ri.valid[i] = v;
+      ri.addr[i] = (uint64_t)(X + ((((int64_t)n * g.H + hi0) * g.W + wi0) * g.C + sc * 8));
     }
   }
 }
 
-template <int BN, bool STATS>
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BM, int BN, int WM, bool STATS>
 __global__ __launch_bounds__(NT) void conv3x3_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Wt, __bf16* __restrict__ Y, Geo g,
     int ntn, int64_t ntm, const float* __restrict__ shift, float* __restrict__ partial) {
-  constexpr int WTN = BN / 2, WTM = BM / 2;
+  constexpr int WN = 4 / WM;
+  constexpr int A_CH = BM * 8 / NT;               // 16-byte chunks per thread per A stage
+  constexpr int WTN = BN / WN, WTM = BM / WM;
   constexpr int TN = WTN / 16, TM = WTM / 16;
   constexpr int B_CH = BN * 8 / NT;
+  constexpr int LPS = A_CH + B_CH;                // glds per thread per stage
   constexpr int STAGE = (BM + BN) * BK;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+  constexpr int NS = 3;                           // LDS ring: 2 stages in flight
+  __shared__ __attribute__((aligned(16))) __bf16 smem[NS * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
+  const int wm = wid / WN, wn = wid % WN;
   const int t = remap(blockIdx.x, gridDim.x);
   const int nt = t % ntn;
   const int64_t stream = t / ntn, nstreams = gridDim.x / ntn;
@@ -110,24 +135,26 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(
   const int64_t wrow = (int64_t)9 * g.C;          // filter row length
   const int sc = (tid & 7) ^ ((tid >> 3) & 7);    // swizzled source chunk of this thread
 
-  auto issue = [&](const RowInfo& ri, int kt, int buf) {
-    const int tap = kt / csteps, c0 = (kt - tap * csteps) * BK;
+  uint64_t brow[B_CH];                            // filter rows of this thread
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i)
+    brow[i] = (uint64_t)(Wt + (int64_t)(n0 + i * (NT / 8) + (tid >> 3)) * wrow + sc * 8);
+  const uint64_t zaddr = (uint64_t)(g_zero + (tid & 7) * 4);
+
+  auto issue = [&](const RowInfo<A_CH>& ri, int kt, int buf) {
+    const int tap = kt / csteps, c0 = (kt - tap * csteps) * BK;   // wave-uniform
     const int r = tap / 3, s = tap - r * 3;
+    const int64_t offa = (((int64_t)r * g.W + s) * g.C + c0) * 2;
+    const int64_t offb = ((int64_t)tap * g.C + c0) * 2;
     __bf16* As = smem + buf * STAGE;
     __bf16* Bs = As + BM * BK;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      const int hi = ri.hi0[i] + r, wi = ri.wi0[i] + s;
-      const bool ok = (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-      const void* src = ok ? (const void*)(X + ri.base[i] + ((int64_t)r * g.W + s) * g.C + c0 + sc * 8)
-                           : (const void*)(g_zero + (tid & 7) * 4);
-      glds16(src, As + (i * NT + wid * 64) * 8);
+      const uint64_t a = ((ri.valid[i] >> tap) & 1u) ? ri.addr[i] + offa : zaddr;
+      glds16((const void*)a, As + (i * NT + wid * 64) * 8);
     }
 #pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int row = i * (NT / 8) + (tid >> 3);
-      glds16(Wt + (int64_t)(n0 + row) * wrow + tap * g.C + c0 + sc * 8, Bs + (i * NT + wid * 64) * 8);
-    }
+    for (int i = 0; i < B_CH; ++i) glds16((const void*)(brow[i] + offb), Bs + (i * NT + wid * 64) * 8);
   };
 
   const int gq = lane >> 4, rl = lane & 15;
@@ -147,75 +174,90 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(
 #pragma unroll
     for (int b = 0; b < TM; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
+  // Step j computes from ring slot j % NS while the loads of steps j+1 and j+2 are
+  // in flight; one raw barrier per step, after a COUNTED vmcnt wait that retires only
+  // step j's loads (loads retire in order, so "<= LPS outstanding" with step j+2's
+  // LPS loads issued last means step j's — and j+1's predecessors — landed; epilogue
+  // stores in between do not disturb the count), so the in-flight loads survive it.
+  // Tiles are the outer loop so the accumulators stay in AGPRs through the K loop.
   int64_t mt = stream;
   if (mt < ntm) {
-    RowInfo cur, nxt;
-    row_info(g, mt * BM, tid, cur);
-    issue(cur, 0, 0);
-    __syncthreads();
-    int kt = 0, buf = 0;
+    RowInfo<A_CH> iri;
+    row_info(g, X, mt * BM, tid, sc, iri);
+    int64_t imt = mt;          // (tile, step) of the last issued stage
+    int ikt = 0;
+    int islot = 0;
+    issue(iri, 0, 0);
+    auto issue_next = [&]() -> bool {
+      int k2 = ikt + 1;
+      int64_t m2 = imt;
+      if (k2 == KT) { k2 = 0; m2 += nstreams; }
+      if (m2 >= ntm) return false;
+      if (m2 != imt) row_info(g, X, m2 * BM, tid, sc, iri);
+      islot = islot + 1 == NS ? 0 : islot + 1;
+      issue(iri, k2, islot);
+      imt = m2;
+      ikt = k2;
+      return true;
+    };
+    bool ahead = issue_next();      // stage of step 1 in flight
+    int slot = 0;
     while (true) {
-      int kt2 = kt + 1;
-      int64_t mt2 = mt;
-      if (kt2 == KT) {
-        kt2 = 0;
-        mt2 += nstreams;
-        if (mt2 < ntm) row_info(g, mt2 * BM, tid, nxt);
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      for (int kt = 0; kt < KT; ++kt) {
+        if (ahead) wait_vm<LPS>(); else wait_vm<0>();
+        raw_barrier();          // this step's stage is visible to all; the oldest slot is free
+        ahead = issue_next();
+        const __bf16* As = smem + slot * STAGE;
+        const __bf16* Bs = As + BM * BK;
+#pragma unroll
+        for (int kk = 0; kk < BK / 32; ++kk) {
+          const int ch = kk * 4 + gq;
+          bf16x8 wf[TN], af[TM];
+#pragma unroll
+          for (int a = 0; a < TN; ++a)
+            wf[a] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WTN + a * 16 + rl, ch));
+#pragma unroll
+          for (int b = 0; b < TM; ++b)
+            af[b] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WTM + b * 16 + rl, ch));
+#pragma unroll
+          for (int a = 0; a < TN; ++a)
+#pragma unroll
+            for (int b = 0; b < TM; ++b) acc[a][b] = mfma(wf[a], af[b], acc[a][b]);
+        }
+        slot = slot + 1 == NS ? 0 : slot + 1;
       }
-      const bool more = mt2 < ntm;
-      if (more) issue(kt2 == 0 ? nxt : cur, kt2, buf ^ 1);
-      const __bf16* As = smem + buf * STAGE;
-      const __bf16* Bs = As + BM * BK;
+      // tile done: store (+ statistics) while the next tile's first loads fly
+      const int64_t m0 = mt * BM;
 #pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
-        const int ch = kk * 4 + gq;
-        bf16x8 wf[TN], af[TM];
+      for (int b = 0; b < TM; ++b) {
+        const int64_t row = m0 + wm * WTM + b * 16 + rl;
+        if (row < g.M) {
 #pragma unroll
-        for (int a = 0; a < TN; ++a)
-          wf[a] = *reinterpret_cast<const bf16x8*>(Bs + swz(wn * WTN + a * 16 + rl, ch));
+          for (int a = 0; a < TN; ++a) {
+            const f32x4v v = acc[a][b];
+            const int col = n0 + wn * WTN + a * 16 + 4 * gq;
+            *reinterpret_cast<u32x2*>(Y + row * g.K + col) =
+                u32x2{cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3])};
+            if (STATS) {
 #pragma unroll
-        for (int b = 0; b < TM; ++b)
-          af[b] = *reinterpret_cast<const bf16x8*>(As + swz(wm * WTM + b * 16 + rl, ch));
-#pragma unroll
-        for (int a = 0; a < TN; ++a)
-#pragma unroll
-          for (int b = 0; b < TM; ++b) acc[a][b] = mfma(wf[a], af[b], acc[a][b]);
-      }
-      if (kt == KT - 1) {      // tile done: store (+ statistics) while the next loads fly
-        const int64_t m0 = mt * BM;
-#pragma unroll
-        for (int b = 0; b < TM; ++b) {
-          const int64_t row = m0 + wm * WTM + b * 16 + rl;
-          if (row < g.M) {
-#pragma unroll
-            for (int a = 0; a < TN; ++a) {
-              const f32x4v v = acc[a][b];
-              const int col = n0 + wn * WTN + a * 16 + 4 * gq;
-              *reinterpret_cast<u32x2*>(Y + row * g.K + col) =
-                  u32x2{cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3])};
-              if (STATS) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  const float d = round_bf16(v[r]) - sh[a][r];
-                  s1[a][r] += d;
-                  s2[a][r] += d * d;
-                }
+              for (int r = 0; r < 4; ++r) {
+                const float d = round_bf16(v[r]) - sh[a][r];
+                s1[a][r] += d;
+                s2[a][r] += d * d;
               }
             }
           }
         }
-#pragma unroll
-        for (int a = 0; a < TN; ++a)
-#pragma unroll
-          for (int b = 0; b < TM; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
       }
-      __syncthreads();         // next stage landed (vmcnt drained) and this one is consumed
-      if (!more) break;
-      if (kt2 == 0) cur = nxt;
-      kt = kt2;
-      mt = mt2;
-      buf ^= 1;
+      mt += nstreams;
+      if (mt >= ntm) break;
     }
+    wait_vm<0>();
+    __syncthreads();
   }
   if (!STATS) return;
 #pragma unroll
@@ -228,31 +270,51 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(
         s2[a][r] += __shfl_xor(s2[a][r], o, kWave);
       }
   __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);      // [2][2 (wm)][BN]
+  float* red = reinterpret_cast<float*>(smem);      // [2][WM][BN]
   if (rl == 0) {
 #pragma unroll
     for (int a = 0; a < TN; ++a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = wn * WTN + a * 16 + 4 * gq + r;
-        red[(0 * 2 + wm) * BN + c] = s1[a][r];
-        red[(1 * 2 + wm) * BN + c] = s2[a][r];
+        red[(0 * WM + wm) * BN + c] = s1[a][r];
+        red[(1 * WM + wm) * BN + c] = s2[a][r];
       }
   }
   __syncthreads();
   if (stream >= ntm) return;
   for (int v = tid; v < 2 * BN; v += NT) {
     const int k = v / BN, c = v - k * BN;
-    partial[(stream * 2 + k) * g.K + n0 + c] = red[(k * 2 + 0) * BN + c] + red[(k * 2 + 1) * BN + c];
+    float acc_s = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) acc_s += red[(k * WM + w) * BN + c];
+    partial[(stream * 2 + k) * g.K + n0 + c] = acc_s;
   }
+}
+
+// tile configs: BN = 128 -> 128 x 128 (2 x 2 waves); BN = 64 -> 256 x 64 (4 x 1 waves)
+template <int BN, bool STATS>
+struct Cfg;
+template <bool STATS>
+struct Cfg<128, STATS> {
+  static constexpr int BM = 128, WM = 2;
+};
+template <bool STATS>
+struct Cfg<64, STATS> {
+  static constexpr int BM = 256, WM = 4;
+};
+
+template <int BN, bool STATS>
+static const void* kernel_ptr() {
+  return (const void*)&conv3x3_kernel<Cfg<BN, STATS>::BM, BN, Cfg<BN, STATS>::WM, STATS>;
 }
 
 template <int BN, bool STATS>
 static int64_t streams_for(int64_t ntm, int ntn) {
   static int per = [] {
     int v = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, (const void*)&conv3x3_kernel<BN, STATS>,
-                                                     NT, 0) != hipSuccess || v < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel_ptr<BN, STATS>(), NT, 0) !=
+            hipSuccess || v < 1)
       v = 1;
     return v;
   }();
@@ -277,9 +339,8 @@ static int conv_bn_of(int K) { return K % 128 == 0 ? 128 : 64; }
 
 int64_t mv_conv3x3_partials(int64_t M, int K) {
   using namespace mv::conv;
-  const int bn = conv_bn_of(K);
-  const int64_t ntm = (M + BM - 1) / BM;
-  return bn == 128 ? streams_for<128, true>(ntm, K / 128) : streams_for<64, true>(ntm, K / 64);
+  if (conv_bn_of(K) == 128) return streams_for<128, true>((M + 127) / 128, K / 128);
+  return streams_for<64, true>((M + 255) / 256, K / 64);
 }
 
 bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int C, int K,
@@ -295,16 +356,17 @@ bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int 
   g.Ho = (H - 1) / stride + 1;
   g.Wo = (W - 1) / stride + 1;
   g.M = (int64_t)N * g.Ho * g.Wo;
-  const int64_t ntm = (g.M + BM - 1) / BM;
   const __bf16* X = (const __bf16*)x;
   const __bf16* Wt = (const __bf16*)w;
   __bf16* Y = (__bf16*)y;
-#define MV_LAUNCH(BNV, ST)                                                                      \
-  {                                                                                             \
-    const int ntn = K / BNV;                                                                    \
-    const int64_t ns = streams_for<BNV, ST>(ntm, ntn);                                          \
-    hipLaunchKernelGGL((conv3x3_kernel<BNV, ST>), dim3((unsigned)(ns * ntn)), dim3(NT), 0, st, X, \
-                       Wt, Y, g, ntn, ntm, shift, partial);                                     \
+#define MV_LAUNCH(BNV, ST)                                                                     \
+  {                                                                                            \
+    constexpr int BMV = Cfg<BNV, ST>::BM, WMV = Cfg<BNV, ST>::WM;                              \
+    const int64_t ntm = (g.M + BMV - 1) / BMV;                                                 \
+    const int ntn = K / BNV;                                                                   \
+    const int64_t ns = streams_for<BNV, ST>(ntm, ntn);                                         \
+    hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, ST>), dim3((unsigned)(ns * ntn)), dim3(NT), \
+                       0, st, X, Wt, Y, g, ntn, ntm, shift, partial);                          \
   }
   if (conv_bn_of(K) == 128) {
     if (partial) MV_LAUNCH(128, true) else MV_LAUNCH(128, false)
