@@ -22,7 +22,9 @@
 // the query = row index of the S tile need no data movement); dQ = dS K sums
 // over keys, so dS goes through LDS once and each key block writes its own fp32
 // dQ partial (plain stores, no atomics: deterministic), reduced by a small
-// kernel.  Dropout masks are regenerated from a counter hash of
+// kernel — or, for s <= 128, bwd_short_kernel: one 8-wave workgroup per (b, h)
+// covering every key, dQ written once in bf16 and delta computed in-kernel.
+// Dropout masks are regenerated from a counter hash of
 // (seed, b*h, query, key) in both passes.
 #include "mv_common.h"
 #include "mv_attn.h"
@@ -420,6 +422,192 @@ __global__ __launch_bounds__(256) void bwd_kernel(AttnParams p, const __bf16* __
   (void)nkb;
 }
 
+// Short sequences (s <= 128, BERT pre-training's 128): ONE workgroup of 8 waves per
+// (b, h) owns all (up to 2) key blocks — waves 0-3 keys 0-63, waves 4-7 keys 64-127 —
+// so dQ = dS K sums over every key inside the workgroup and is written once in bf16
+// (no fp32 partials, no dq_reduce pass), delta = rowsum(dO * O) is computed in the
+// query-block prologue (no delta pass), and each Q / dO block is staged once for both
+// key halves.
+__global__ __launch_bounds__(512) void bwd_short_kernel(AttnParams p,
+                                                         const __bf16* __restrict__ out,
+                                                         const __bf16* __restrict__ dout,
+                                                         __bf16* __restrict__ dqkv) {
+  constexpr int SK = 2 * KB;     // keys per workgroup
+  const int bh = blockIdx.x;
+  const int bi = bh / p.h, hi = bh % p.h;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
+  const int kh = w >> 2, wq = w & 3;
+  const int k0 = kh * KB + wq * 16;
+  const int64_t tok = 3LL * p.h * D;
+  const int64_t otok = (int64_t)p.h * D;
+  const __bf16* Qb = ((const __bf16*)p.qkv) + (int64_t)bi * p.s * tok + (int64_t)hi * D;
+  const __bf16* Kb = Qb + (int64_t)p.h * D;
+  const __bf16* Vb = Qb + 2LL * p.h * D;
+  const __bf16* dOb = dout + (int64_t)bi * p.s * otok + (int64_t)hi * D;
+  const __bf16* Ob = out + (int64_t)bi * p.s * otok + (int64_t)hi * D;
+
+  __shared__ __attribute__((aligned(16))) __bf16 Qs[QB][D + PAD];
+  __shared__ __attribute__((aligned(16))) __bf16 Qt[D][QB + PAD];
+  __shared__ __attribute__((aligned(16))) __bf16 dOs[QB][D + PAD];
+  __shared__ __attribute__((aligned(16))) __bf16 dOt[D][QB + PAD];
+  __shared__ __attribute__((aligned(16))) __bf16 dSs[QB][SK + PAD];
+  __shared__ __attribute__((aligned(16))) __bf16 Kt[D][SK + PAD];
+  __shared__ float lse_s[QB], del_s[QB];
+
+  bf16x8 kf[2], vf[2];
+  {
+    const int key = k0 + c;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[ks] = key < p.s ? ld_b128(Kb + (int64_t)key * tok + 32 * ks + 8 * g) : zero8();
+      vf[ks] = key < p.s ? ld_b128(Vb + (int64_t)key * tok + 32 * ks + 8 * g) : zero8();
+    }
+  }
+  {  // K^T of all SK keys for dQ = dS K
+    const int t = threadIdx.x, key = t >> 2, d0 = (t & 3) * 16;
+    bf16x8 a = zero8(), b2 = zero8();
+    if (key < p.s) {
+      a = ld_b128(Kb + (int64_t)key * tok + d0);
+      b2 = ld_b128(Kb + (int64_t)key * tok + d0 + 8);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      Kt[d0 + j][key] = a[j];
+      Kt[d0 + 8 + j][key] = b2[j];
+    }
+  }
+  f32x4v dVt[4], dKt[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    dVt[n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    dKt[n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  }
+  const float inv_keep = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+  const float qscale = p.scale_log2 / LOG2E;   // 1/sqrt(D)
+  const int keyc = k0 + c;
+  const float kbias = (p.mask && keyc < p.s) ? p.mask[(int64_t)bi * p.s + keyc] * LOG2E : 0.f;
+
+  for (int qb0 = 0; qb0 < p.s; qb0 += QB) {
+    __syncthreads();
+    if (threadIdx.x < 256) {   // Q / dO tiles, row-major and transposed
+      const int t = threadIdx.x, row = t >> 2, d0 = (t & 3) * 16;
+      const int qg = qb0 + row;
+      bf16x8 q0v = zero8(), q1v = zero8(), o0 = zero8(), o1 = zero8();
+      if (qg < p.s) {
+        q0v = ld_b128(Qb + (int64_t)qg * tok + d0);
+        q1v = ld_b128(Qb + (int64_t)qg * tok + d0 + 8);
+        o0 = ld_b128(dOb + (int64_t)qg * otok + d0);
+        o1 = ld_b128(dOb + (int64_t)qg * otok + d0 + 8);
+      }
+      *reinterpret_cast<bf16x8*>(&Qs[row][d0]) = q0v;
+      *reinterpret_cast<bf16x8*>(&Qs[row][d0 + 8]) = q1v;
+      *reinterpret_cast<bf16x8*>(&dOs[row][d0]) = o0;
+      *reinterpret_cast<bf16x8*>(&dOs[row][d0 + 8]) = o1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Qt[d0 + j][row] = q0v[j];
+        Qt[d0 + 8 + j][row] = q1v[j];
+        dOt[d0 + j][row] = o0[j];
+        dOt[d0 + 8 + j][row] = o1[j];
+      }
+      if (t < QB) {
+        const int qq = qb0 + t;
+        lse_s[t] = qq < p.s ? p.lse[(int64_t)bh * p.s + qq] : INFINITY;
+      }
+    } else {                   // delta = rowsum(dO * O): 4 lanes x 16 dims per query
+      const int u = threadIdx.x - 256, row = u >> 2, d0 = (u & 3) * 16;
+      const int qg = qb0 + row;
+      float acc = 0.f;
+      if (qg < p.s) {
+        float a[8], e[8];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          load8(Ob + (int64_t)qg * otok + d0 + 8 * hh, a);
+          load8(dOb + (int64_t)qg * otok + d0 + 8 * hh, e);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc += a[j] * e[j];
+        }
+      }
+      acc += __shfl_xor(acc, 1, 64);
+      acc += __shfl_xor(acc, 2, 64);
+      if ((u & 3) == 0) del_s[row] = acc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {         // 32-query chunks
+      float zc[2][4], dsc[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int qt = 2 * ch + u;
+        f32x4v sacc = {0.f, 0.f, 0.f, 0.f}, pacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          sacc = mfma(ld_b128(&Qs[16 * qt + c][32 * ks + 8 * g]), kf[ks], sacc);
+          pacc = mfma(ld_b128(&dOs[16 * qt + c][32 * ks + 8 * g]), vf[ks], pacc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = 16 * qt + 4 * g + r;
+          float pr = 0.f;
+          if (keyc < p.s) pr = exp2f(sacc[r] * p.scale_log2 + kbias - lse_s[ql]);
+          float z = pr, dzd = pacc[r];
+          if (p.p_drop > 0.f) {
+            const bool kp = keep_elem(p.seed, bh, (uint32_t)(qb0 + ql), (uint32_t)keyc, p.thresh);
+            z = kp ? pr * inv_keep : 0.f;
+            dzd = kp ? dzd * inv_keep : 0.f;
+          }
+          const float ds = pr * (dzd - del_s[ql]);
+          zc[u][r] = z;
+          dsc[u][r] = ds;
+          dSs[ql][kh * KB + wq * 16 + c] = (__bf16)ds;
+        }
+      }
+      float zb[8] = {zc[0][0], zc[0][1], zc[0][2], zc[0][3], zc[1][0], zc[1][1], zc[1][2], zc[1][3]};
+      float sb[8] = {dsc[0][0], dsc[0][1], dsc[0][2], dsc[0][3],
+                     dsc[1][0], dsc[1][1], dsc[1][2], dsc[1][3]};
+      const bf16x8 zf = pack8(zb), sf = pack8(sb);
+      const int qa = 32 * ch + 4 * g, qbb = 32 * ch + 16 + 4 * g;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        dVt[n] = mfma(ld_2x4(&dOt[16 * n + c][qa], &dOt[16 * n + c][qbb]), zf, dVt[n]);
+        dKt[n] = mfma(ld_2x4(&Qt[16 * n + c][qa], &Qt[16 * n + c][qbb]), sf, dKt[n]);
+      }
+    }
+    __syncthreads();
+    // dQ[64 q, 64 d] = dS[64, SK] K[SK, 64]: wave -> query tile w&3, d tiles 2(w>>2)+{0,1}
+    {
+      const int qt = w & 3;
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        const int n = 2 * (w >> 2) + nn;
+        f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < SK / 32; ++ks)
+          acc = mfma(ld_b128(&dSs[16 * qt + c][32 * ks + 8 * g]),
+                     ld_b128(&Kt[16 * n + c][32 * ks + 8 * g]), acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = qb0 + 16 * qt + 4 * g + r;
+          if (q < p.s)
+            dqkv[((int64_t)bi * p.s + q) * tok + (int64_t)hi * D + 16 * n + c] =
+                (__bf16)(acc[r] * qscale);
+        }
+      }
+    }
+  }
+  if (keyc < p.s) {
+    __bf16* dk = dqkv + ((int64_t)bi * p.s + keyc) * tok + (int64_t)p.h * D + (int64_t)hi * D;
+    __bf16* dv = dk + (int64_t)p.h * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dk[16 * n + 4 * g + r] = (__bf16)(dKt[n][r] * qscale);
+        dv[16 * n + 4 * g + r] = (__bf16)dVt[n][r];
+      }
+  }
+}
+
 __global__ __launch_bounds__(256) void dq_reduce_kernel(const float* __restrict__ dq_part,
                                                          __bf16* __restrict__ dqkv, int nkb,
                                                          int b, int s, int h, float scale) {
@@ -453,6 +641,11 @@ void mv_attn_fwd(const AttnParams& p, hipStream_t st) {
 
 void mv_attn_bwd(const AttnParams& p, const void* out, const void* dout, float* delta,
                  float* dq_part, void* dqkv, hipStream_t st) {
+  if (p.s <= 2 * KB) {   // one workgroup per (b, h): no delta / dq_reduce passes
+    hipLaunchKernelGGL(bwd_short_kernel, dim3(p.b * p.h), dim3(512), 0, st, p, (const __bf16*)out,
+                       (const __bf16*)dout, (__bf16*)dqkv);
+    return;
+  }
   const int64_t rows = (int64_t)p.b * p.s * p.h;
   static_assert(D == 64, "delta_kernel maps 8 lanes x 8 elements onto a row");
   hipLaunchKernelGGL(delta_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, st,

@@ -554,8 +554,10 @@ at::Tensor attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor 
   p.lse = lse.data_ptr<float>();
   auto fo = qkv.options().dtype(at::kFloat);
   const int nkb = (p.s + 63) / 64;
-  at::Tensor delta = at::empty({p.b, p.h, p.s}, fo);
-  at::Tensor dq_part = at::empty({(int64_t)nkb * p.b * p.s * p.h * 64}, fo);
+  // s <= 128 runs the single-workgroup-per-(b, h) kernel: no delta / dQ partials
+  const bool short_seq = p.s <= 128;
+  at::Tensor delta = at::empty({short_seq ? 1 : (int64_t)p.b * p.h * p.s}, fo);
+  at::Tensor dq_part = at::empty({short_seq ? 1 : (int64_t)nkb * p.b * p.s * p.h * 64}, fo);
   at::Tensor dqkv = at::empty_like(qkv);
   mv_attn_bwd(p, out.data_ptr(), dout.data_ptr(), delta.data_ptr<float>(),
               dq_part.data_ptr<float>(), dqkv.data_ptr(), cur_stream());
