@@ -839,7 +839,7 @@ int64_t gemm_bwd_partials(int64_t M, int64_t N, int64_t K, int64_t bn) {
 // : 0 is written to dz, returns the fp32 [P, 2, N] partials (sum dz, sum dz (x - mean)).
 at::Tensor gemm_nt_bn_bwd(at::Tensor a, at::Tensor b, at::Tensor dz,
                           c10::optional<at::Tensor> dy2, at::Tensor mask, at::Tensor x,
-                          at::Tensor vec, int64_t bn) {
+                          at::Tensor vec, int64_t bn, int64_t dy2_stride, int64_t H, int64_t W) {
   for (const at::Tensor* t : {&a, &b, &dz, &x})
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous(),
                 "gemm_nt_bn_bwd: A, B, dz, x must be contiguous bf16 GPU tensors");
@@ -856,14 +856,24 @@ at::Tensor gemm_nt_bn_bwd(at::Tensor a, at::Tensor b, at::Tensor dz,
   TORCH_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() &&
                   vec.numel() == 4 * N, "gemm_nt_bn_bwd: saved stats must be fp32 [4, N]");
   const void* d2 = nullptr;
+  TORCH_CHECK(dy2_stride >= 1, "gemm_nt_bn_bwd: bad dy2 stride");
   if (dy2.has_value() && dy2->defined()) {
     const bool ok_layout = dy2->dim() == 4
                                ? dy2->size(1) == N &&
                                      dy2->is_contiguous(at::MemoryFormat::ChannelsLast)
                                : dy2->is_contiguous();
-    TORCH_CHECK(dy2->is_cuda() && dy2->scalar_type() == at::kBFloat16 && ok_layout &&
-                    dy2->numel() == M * N,
-                "gemm_nt_bn_bwd: dy2 must be bf16 [M, N] (NHWC-contiguous)");
+    TORCH_CHECK(dy2->is_cuda() && dy2->scalar_type() == at::kBFloat16 && ok_layout,
+                "gemm_nt_bn_bwd: dy2 must be bf16 [*, N] (NHWC-contiguous)");
+    if (dy2_stride == 1) {
+      TORCH_CHECK(dy2->numel() == M * N, "gemm_nt_bn_bwd: dy2 must be [M, N]");
+    } else {
+      TORCH_CHECK(H > 0 && W > 0 && M % (H * W) == 0 && M < (int64_t(1) << 31),
+                  "gemm_nt_bn_bwd: strided dy2 needs M = n*H*W < 2^31");
+      const int64_t s = dy2_stride, hs = (H + s - 1) / s, ws = (W + s - 1) / s;
+      TORCH_CHECK(dy2->dim() == 4 && dy2->size(0) == M / (H * W) && dy2->size(2) == hs &&
+                      dy2->size(3) == ws,
+                  "gemm_nt_bn_bwd: strided dy2 must be [n, N, ceil(H/s), ceil(W/s)]");
+    }
     d2 = dy2->data_ptr();
   }
   for (const at::Tensor* t : {&b, &dz, &x, &mask, &vec})
@@ -872,7 +882,8 @@ at::Tensor gemm_nt_bn_bwd(at::Tensor a, at::Tensor b, at::Tensor dz,
   at::Tensor partial = at::empty({P, 2, N}, a.options().dtype(at::kFloat));
   TORCH_CHECK(mv_gemm_nt_bn_bwd(a.data_ptr(), b.data_ptr(), dz.data_ptr(), M, (int)N, (int)K, d2,
                                 mask.data_ptr(), x.data_ptr(), vec[0].data_ptr<float>(),
-                                partial.data_ptr<float>(), (int)bn, cur_stream()),
+                                partial.data_ptr<float>(), (int)bn, cur_stream(), (int)dy2_stride,
+                                (int)H, (int)W),
               "gemm_nt_bn_bwd: launch failed");
   return partial;
 }
@@ -1001,7 +1012,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_nt_bn_bwd", &gemm_nt_bn_bwd,
         "1x1-conv data-gradient GEMM with the producing BN's add+ReLU backward reduce fused",
         py::arg("a"), py::arg("b"), py::arg("dz"), py::arg("dy2"), py::arg("mask"), py::arg("x"),
-        py::arg("vec"), py::arg("bn") = 0);
+        py::arg("vec"), py::arg("bn") = 0, py::arg("dy2_stride") = 1, py::arg("H") = 1,
+        py::arg("W") = 1);
   m.def("gemm_bwd_partials", &gemm_bwd_partials, "partial rows of gemm_nt_bn_bwd (-1: unsupported)",
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bn") = 0);
   m.def("bn_bwd_from_partials", &bn_bwd_from_partials,

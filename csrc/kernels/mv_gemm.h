@@ -16,6 +16,9 @@ void mv_gemm_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
 // (sum d, sum d * (x - mean)) with P = mv_gemm_bwd_partials(M, N, K, bn); bn = the
 // column-tile width (0: default)
 int64_t mv_gemm_bwd_partials(int64_t M, int N, int K, int bn);
+// dy2_stride > 1: dy2 is [*, ceil(H/s), ceil(W/s), N] on the stride grid of the [*, H, W]
+// rows (added where h and w are multiples of s)
 bool mv_gemm_nt_bn_bwd(const void* A, const void* B, void* DZ, int64_t M, int N, int K,
                        const void* dy2, const void* mask, const void* x, const float* mean,
-                       float* partial, int bn, hipStream_t st);
+                       float* partial, int bn, hipStream_t st, int dy2_stride = 1, int H = 1,
+                       int W = 1);

@@ -231,6 +231,10 @@ struct BwdEpi {
   const uint8_t* mask;    // [M, N/8] bitmask of the forward output > 0
   const __bf16* x;        // [M, N] BN input
   const float* mean;      // [N] saved mean
+  // ds > 1: dy2 lives on the stride-ds grid of the [*, H, W] rows (the input gradient
+  // of a strided 1x1 shortcut conv, ops/bn.py downsample_tap): row (n, h, w) adds
+  // dy2[n, h/ds, w/ds] when h and w are multiples of ds
+  int ds, H, W;
 };
 
 // raw 16-/8-byte loads of NC consecutive bf16 (issued early, unpacked in the epilogue)
@@ -316,7 +320,25 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       for (int b = 0; b < TM; ++b) {
         int64_t row = mt * BM + b * 16 + rl;
         row = row < M ? row : M - 1;
-        if (be.dy2) ld_raw<NC>(be.dy2 + row * N + cbase, e2[b]);
+        if (be.dy2) {
+          int64_t r2 = row;
+          bool has = true;
+          if (be.ds > 1) {     // rows < 2^31 (checked by the binding)
+            const uint32_t m = (uint32_t)row, hw = (uint32_t)(be.H * be.W);
+            const uint32_t n = m / hw, rem = m - n * hw;
+            const uint32_t h = rem / (uint32_t)be.W, w = rem - h * (uint32_t)be.W;
+            const uint32_t hs = ((uint32_t)be.H + be.ds - 1) / be.ds;
+            const uint32_t ws = ((uint32_t)be.W + be.ds - 1) / be.ds;
+            has = h % be.ds == 0 && w % be.ds == 0;
+            r2 = ((int64_t)n * hs + h / be.ds) * ws + w / be.ds;
+          }
+          if (has) {
+            ld_raw<NC>(be.dy2 + r2 * N + cbase, e2[b]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < NC / 2; ++j) e2[b][j] = 0u;
+          }
+        }
         ld_raw<NC>(be.x + row * N + cbase, ex[b]);
         const uint8_t* mp = be.mask + row * (N / 8) + cbase / 8;
         if constexpr (NC == 4) em[b] = (uint32_t)mp[0] >> (cbase & 7);
@@ -570,11 +592,12 @@ int64_t mv_gemm_bwd_partials(int64_t M, int N, int K, int req_bn) {
 
 bool mv_gemm_nt_bn_bwd(const void* A, const void* B, void* DZ, int64_t M, int N, int K,
                        const void* dy2, const void* mask, const void* x, const float* mean,
-                       float* partial, int req_bn, hipStream_t st) {
+                       float* partial, int req_bn, hipStream_t st, int dy2_stride, int H, int W) {
   using namespace mv::gemm;
   int bn;
   if (!bwd_cfg(K, N, req_bn, &bn)) return false;
-  BwdEpi e{(const __bf16*)dy2, (const uint8_t*)mask, (const __bf16*)x, mean};
+  BwdEpi e{(const __bf16*)dy2, (const uint8_t*)mask, (const __bf16*)x, mean,
+           dy2_stride > 1 ? dy2_stride : 1, H, W};
   const __bf16* a = (const __bf16*)A;
   const __bf16* b = (const __bf16*)B;
   __bf16* c = (__bf16*)DZ;

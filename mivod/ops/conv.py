@@ -89,6 +89,8 @@ class _Conv1x1BN(torch.autograd.Function):
     (sum dz, sum dz (x_bn - mean)) ride along, and both are handed to the BN through
     the slot (``slot.pending``) while autograd receives None for x.  The BN backward
     then skips its reduce pass (one full read of dx, dy2, x_bn and a write of dz).
+    A shortcut gradient on a stride grid (stage-entry blocks, ops.bn.downsample_tap) is
+    added on that grid inside the epilogue.
     """
 
     @staticmethod
@@ -122,16 +124,17 @@ class _Conv1x1BN(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             slot, ctx.slot = ctx.slot, None
             if (slot is not None and slot.bn is not None and slot.grad is not None
-                    and slot.stride == 1 and slot.pending is None):
+                    and slot.pending is None):
                 from . import kernels as K
                 n, cin, h, wd = x.shape
                 cout, m = w.shape[0], n * h * wd
                 xb, mask, vec = slot.bn
                 dz = torch.empty_like(x)
+                g2, s2 = slot.take_strided()      # stride > 1: a stage-entry shortcut's grid
                 part = K.native().gemm_nt_bn_bwd(
                     dy.permute(0, 2, 3, 1).reshape(m, cout), w.reshape(cout, cin).t().contiguous(),
-                    dz.permute(0, 2, 3, 1).reshape(m, cin), slot.take(), mask,
-                    xb.permute(0, 2, 3, 1).reshape(m, cin), vec)
+                    dz.permute(0, 2, 3, 1).reshape(m, cin), g2, mask,
+                    xb.permute(0, 2, 3, 1).reshape(m, cin), vec, 0, s2, h, wd)
                 slot.pending = (dz, part)
             else:
                 dx = F.conv2d(dy, _transposed_filter(w))

@@ -142,6 +142,32 @@ def test_gemm_nt_bn_bwd_matches_fp32(cuda, M, K, N, with_dy2):
     assert (dz.float()[~_unpack_mask(mask, N)] == 0).all()
 
 
+@pytest.mark.parametrize("H,W,ds", [(8, 8, 2), (7, 9, 2), (5, 5, 3)])
+def test_gemm_nt_bn_bwd_strided_dy2(cuda, H, W, ds):
+    """dy2 on the stride-ds grid is added at rows whose (h, w) are multiples of ds."""
+    nat = _nat()
+    n, K, N = 3, 128, 256
+    M = n * H * W
+    g = torch.Generator(device=cuda).manual_seed(H * 100 + W + ds)
+    a = torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).to(torch.bfloat16)
+    x = torch.randn(M, N, device=cuda, generator=g).to(torch.bfloat16)
+    vec = torch.randn(4, N, device=cuda, generator=g)
+    mask = torch.randint(0, 256, (M, N // 8), device=cuda, generator=g, dtype=torch.int32).to(
+        torch.uint8)
+    hs, ws = (H + ds - 1) // ds, (W + ds - 1) // ds
+    dy2 = torch.randn(n, N, hs, ws, device=cuda, generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dz = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    part = nat.gemm_nt_bn_bwd(a, b, dz, dy2, mask, x, vec, 0, ds, H, W)
+    full = torch.zeros(n, N, H, W, device=cuda)
+    full[:, :, ::ds, ::ds] = dy2.float()
+    d = (a.float() @ b.float().t()).to(torch.bfloat16).float() + full.permute(0, 2, 3, 1).reshape(M, N)
+    d = torch.where(_unpack_mask(mask, N), d, torch.zeros_like(d))
+    torch.testing.assert_close(dz.float(), d, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(part.sum(0)[0], d.sum(0), rtol=1e-2, atol=1e-1)
+
+
 def test_gemm_nt_bn_bwd_rejects_unsupported(cuda):
     nat = _nat()
     M, K, N = 64, 512, 128          # K = 512: no streaming kernel
@@ -220,7 +246,8 @@ def test_resnet_bwd_fusion_matches_unfused(cuda, monkeypatch):
         monkeypatch.setenv("MIVOD_CONV_BN_BWD_FUSE", fuse)
         out[fuse] = grads(copy.deepcopy(base), x)
         if fuse == "1":
-            assert len(calls) == 3, calls     # layer1.1, layer2.1, layer3.1
+            # layer1.1, layer2.0 (strided shortcut grad), layer2.1, layer3.0 (strided), layer3.1
+            assert len(calls) == 5, calls
     for k, r in ref.items():
         n = float(r.norm()) + 1e-12
         ef = float((out["1"][k] - r).norm()) / n
