@@ -35,7 +35,6 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BK = 64;              // input channels per K step (one tap)
-constexpr int NT = 256;             // 4 waves
 
 __device__ __attribute__((aligned(16))) uint32_t g_zero[32];   // zero page for padding taps
 
@@ -71,7 +70,7 @@ struct RowInfo {
   uint32_t valid[A_CH];
 };
 
-template <int A_CH>
+template <int A_CH, int NT>
 __device__ __forceinline__ void row_info(const Geo& g, const __bf16* X, int64_t m0, int tid,
                                          int sc, RowInfo<A_CH>& ri) {
 #pragma unroll
@@ -110,11 +109,11 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN, int WM, bool STATS>
-__global__ __launch_bounds__(NT) void conv3x3_kernel(
+template <int BM, int BN, int WM, int WN, bool STATS>
+__global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Wt, __bf16* __restrict__ Y, Geo g,
     int ntn, int64_t ntm, const float* __restrict__ shift, float* __restrict__ partial) {
-  constexpr int WN = 4 / WM;
+  constexpr int NT = WM * WN * 64;
   constexpr int A_CH = BM * 8 / NT;               // 16-byte chunks per thread per A stage
   constexpr int WTN = BN / WN, WTM = BM / WM;
   constexpr int TN = WTN / 16, TM = WTM / 16;
@@ -183,7 +182,7 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(
   int64_t mt = stream;
   if (mt < ntm) {
     RowInfo<A_CH> iri;
-    row_info(g, X, mt * BM, tid, sc, iri);
+    row_info<A_CH, NT>(g, X, mt * BM, tid, sc, iri);
     int64_t imt = mt;          // (tile, step) of the last issued stage
     int ikt = 0;
     int islot = 0;
@@ -193,7 +192,7 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(
       int64_t m2 = imt;
       if (k2 == KT) { k2 = 0; m2 += nstreams; }
       if (m2 >= ntm) return false;
-      if (m2 != imt) row_info(g, X, m2 * BM, tid, sc, iri);
+      if (m2 != imt) row_info<A_CH, NT>(g, X, m2 * BM, tid, sc, iri);
       islot = islot + 1 == NS ? 0 : islot + 1;
       issue(iri, k2, islot);
       imt = m2;
@@ -292,28 +291,31 @@ __global__ __launch_bounds__(NT) void conv3x3_kernel(
   }
 }
 
-// tile configs: BN = 128 -> 128 x 128 (2 x 2 waves); BN = 64 -> 256 x 64 (4 x 1 waves)
+// tile configs (8 waves): BN = 128 -> 256 x 128 (4 x 2 waves of 64 x 64); BN = 64 -> 256 x 64
+// (4 x 2 waves of 64 x 32)
 template <int BN, bool STATS>
 struct Cfg;
 template <bool STATS>
 struct Cfg<128, STATS> {
-  static constexpr int BM = 128, WM = 2;
+  static constexpr int BM = 256, WM = 4, WN = 2;
 };
 template <bool STATS>
 struct Cfg<64, STATS> {
-  static constexpr int BM = 256, WM = 4;
+  static constexpr int BM = 256, WM = 4, WN = 2;
 };
 
 template <int BN, bool STATS>
 static const void* kernel_ptr() {
-  return (const void*)&conv3x3_kernel<Cfg<BN, STATS>::BM, BN, Cfg<BN, STATS>::WM, STATS>;
+  using C = Cfg<BN, STATS>;
+  return (const void*)&conv3x3_kernel<C::BM, BN, C::WM, C::WN, STATS>;
 }
 
 template <int BN, bool STATS>
 static int64_t streams_for(int64_t ntm, int ntn) {
   static int per = [] {
     int v = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel_ptr<BN, STATS>(), NT, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &v, kernel_ptr<BN, STATS>(), Cfg<BN, STATS>::WM * Cfg<BN, STATS>::WN * 64, 0) !=
             hipSuccess || v < 1)
       v = 1;
     return v;
@@ -339,8 +341,9 @@ static int conv_bn_of(int K) { return K % 128 == 0 ? 128 : 64; }
 
 int64_t mv_conv3x3_partials(int64_t M, int K) {
   using namespace mv::conv;
-  if (conv_bn_of(K) == 128) return streams_for<128, true>((M + 127) / 128, K / 128);
-  return streams_for<64, true>((M + 255) / 256, K / 64);
+  if (conv_bn_of(K) == 128)
+    return streams_for<128, true>((M + Cfg<128, true>::BM - 1) / Cfg<128, true>::BM, K / 128);
+  return streams_for<64, true>((M + Cfg<64, true>::BM - 1) / Cfg<64, true>::BM, K / 64);
 }
 
 bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int C, int K,
@@ -361,12 +364,13 @@ bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int 
   __bf16* Y = (__bf16*)y;
 #define MV_LAUNCH(BNV, ST)                                                                     \
   {                                                                                            \
-    constexpr int BMV = Cfg<BNV, ST>::BM, WMV = Cfg<BNV, ST>::WM;                              \
+    constexpr int BMV = Cfg<BNV, ST>::BM, WMV = Cfg<BNV, ST>::WM, WNV = Cfg<BNV, ST>::WN;      \
     const int64_t ntm = (g.M + BMV - 1) / BMV;                                                 \
     const int ntn = K / BNV;                                                                   \
     const int64_t ns = streams_for<BNV, ST>(ntm, ntn);                                         \
-    hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, ST>), dim3((unsigned)(ns * ntn)), dim3(NT), \
-                       0, st, X, Wt, Y, g, ntn, ntm, shift, partial);                          \
+    hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, WNV, ST>), dim3((unsigned)(ns * ntn)),      \
+                       dim3(WMV * WNV * 64),                                                   \
+                       0, st, X, Wt, Y, g, ntn, ntm, shift, partial);                         \
   }
   if (conv_bn_of(K) == 128) {
     if (partial) MV_LAUNCH(128, true) else MV_LAUNCH(128, false)

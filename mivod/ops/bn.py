@@ -395,9 +395,13 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = Fa
     the BN is training with running statistics, and with x's producer BN backward
     reduce run in this conv's data-gradient GEMM when x is a fused BN+add+ReLU output
     (ops.conv.bwd_fusable); the plain composition otherwise."""
-    from .conv import bwd_fusable, conv1x1_bn, stats_fusable
-    fwd = (bn.training and bn.track_running_stats and bn.running_mean is not None
-           and _fusable(x, bn.weight) and stats_fusable(conv, x))
+    from .conv import bwd_fusable, conv1x1_bn, conv3x3_bn, conv3x3_eligible, stats_fusable
+    train_stats = (bn.training and bn.track_running_stats and bn.running_mean is not None
+                   and _fusable(x, bn.weight))
+    if conv3x3_eligible(conv, x):
+        y, part = conv3x3_bn(conv, x, bn.running_mean if train_stats else None, train_stats)
+        return bn(y, residual=residual, relu=relu, stats=part if train_stats else None)
+    fwd = train_stats and stats_fusable(conv, x)
     slot = bwd_fusable(conv, x)
     if fwd or slot is not None:
         y, part = conv1x1_bn(conv, x, bn.running_mean if fwd else None, fwd, slot)

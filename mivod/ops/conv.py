@@ -177,6 +177,83 @@ def conv1x1_stats(m: nn.Conv2d, x: torch.Tensor, shift):
     return _Conv1x1BN.apply(x, m.weight, shift, True, None)
 
 
+# ---------------------------------------------------------------- 3x3 implicit GEMM
+def conv3x3_eligible(m: nn.Conv2d, x: torch.Tensor) -> bool:
+    """3x3 / pad 1 / stride 1-2 convs on channels_last bf16 GPU tensors with channel
+    counts that are multiples of 64 (every ResNet-50 bottleneck conv2)."""
+    return (os.environ.get("MIVOD_CONV3X3", "1") != "0"
+            and x.is_cuda and x.dtype == torch.bfloat16 and m.weight.dtype == torch.bfloat16
+            and m.bias is None and m.groups == 1 and tuple(m.kernel_size) == (3, 3)
+            and tuple(m.padding) == (1, 1) and tuple(m.dilation) == (1, 1)
+            and m.stride[0] == m.stride[1] and m.stride[0] in (1, 2) and m.padding_mode == "zeros"
+            and m.in_channels % 64 == 0 and m.out_channels % 64 == 0 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def _dgrad_on_mivod(cin: int, cout: int) -> bool:
+    """The stride-1 data gradient (a forward 3x3 conv Cout -> Cin) runs on mivod's kernel
+    where it beats MIOpen's forward solver (scripts/micro_conv3x3.py: 64- and 128-channel
+    layers); wider layers keep MIOpen."""
+    return os.environ.get("MIVOD_CONV3X3_DGRAD", "1") != "0" and max(cin, cout) <= 128
+
+
+class _Conv3x3(torch.autograd.Function):
+    """y = conv3x3(x, w, stride, pad 1) on mivod's implicit-GEMM kernel (csrc/kernels/
+    mv_conv.hip), optionally with the following BatchNorm's statistics partials of y
+    around ``shift`` (non-differentiable second output).  Backward: stride-1 data
+    gradient as a forward conv with the flipped, channel-transposed filter (mivod's
+    kernel for <= 128 channels, MIOpen's forward solver otherwise), stride-2 data
+    gradient and the weight gradient from MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, shift, stats):
+        from . import kernels as K
+        nat = K.native()
+        wc = w.contiguous(memory_format=torch.channels_last)
+        if stats:
+            n, _, h, wd = x.shape
+            ho, wo = (h - 1) // stride + 1, (wd - 1) // stride + 1
+            k = w.shape[0]
+            part = torch.empty(nat.conv3x3_partials(n * ho * wo, k), 2, k, dtype=torch.float32,
+                               device=x.device)
+            y = nat.conv3x3(x, wc, stride, shift, part)
+        else:
+            part = torch.empty(0, dtype=torch.float32, device=x.device)
+            y = nat.conv3x3(x, wc, stride)
+        ctx.save_for_backward(x, w)
+        ctx.stride = stride
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        s = ctx.stride
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        if s == 1:
+            if need_x:
+                wt = _transposed_filter(w)
+                if _dgrad_on_mivod(w.shape[1], w.shape[0]):
+                    from . import kernels as K
+                    dx = K.native().conv3x3(dy, wt, 1)
+                else:
+                    dx = F.conv2d(dy, wt, None, 1, 1)
+            if need_w:
+                _, dw, _ = torch.ops.aten.convolution_backward(
+                    dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
+        else:
+            dx, dw, _ = torch.ops.aten.convolution_backward(
+                dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [need_x, need_w, False])
+        return dx, dw, None, None, None
+
+
+def conv3x3_bn(m: nn.Conv2d, x: torch.Tensor, shift, stats: bool):
+    """(y, partial) — see _Conv3x3; ``shift`` is the BN's running mean (stats only)."""
+    return _Conv3x3.apply(x, m.weight, int(m.stride[0]), shift, stats)
+
+
 class Conv2d(nn.Conv2d):
     """``nn.Conv2d`` (same parameters / state_dict) with the forward-conv dgrad."""
 

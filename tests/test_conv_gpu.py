@@ -53,3 +53,53 @@ def test_conv3x3_rejects_bad_shapes(cuda):
     w = _cl(torch.zeros(64, 64, 3, 3, device=cuda, dtype=torch.bfloat16))
     with pytest.raises(RuntimeError):
         nat.conv3x3(x, w, 3)
+
+
+@pytest.mark.parametrize("c,k,s", [(64, 64, 1), (128, 128, 2), (128, 128, 1), (256, 256, 1)])
+def test_conv3x3_bn_matches_unfused(cuda, monkeypatch, c, k, s):
+    """conv3x3 -> BN+ReLU through mivod's kernel (statistics in the epilogue, own or
+    MIOpen data gradient) vs MIOpen + the separate BN statistics pass."""
+    import copy
+
+    from mivod.ops.bn import BatchNorm2d, conv_bn
+    from mivod.ops.conv import Conv2d
+    torch.manual_seed(0)
+    conv = Conv2d(c, k, 3, stride=s, padding=1, bias=False).to(cuda).to(torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    bn = BatchNorm2d(k).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-0.2, 0.2)
+    x0 = _cl(torch.randn(4, c, 14, 14, device=cuda).to(torch.bfloat16))
+    outs = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("MIVOD_CONV3X3", on)
+        c2, b2 = copy.deepcopy(conv), copy.deepcopy(bn)
+        x = x0.clone().requires_grad_()
+        y = conv_bn(c2, b2, x, relu=True)
+        y.float().square().mean().backward()
+        outs.append((y.detach().float(), x.grad.float(), c2.weight.grad.float(), b2.weight.grad,
+                     b2.running_mean.clone(), b2.running_var.clone()))
+    (yf, dxf, dwf, dgf, rmf, rvf), (yu, dxu, dwu, dgu, rmu, rvu) = outs
+    torch.testing.assert_close(rmf, rmu, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rvf, rvu, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(yf, yu, rtol=2e-2, atol=2e-2)
+    for a, b in ((dxf, dxu), (dwf, dwu), (dgf, dgu)):
+        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2 * float(b.abs().max()))
+
+
+def test_resnet_bottleneck_uses_conv3x3(cuda):
+    from mivod.models.resnet import ResNet, to_mixed_bf16
+    m = to_mixed_bf16(ResNet((1, 1, 1, 1), num_classes=10)).to(cuda)
+    x = _cl(torch.rand(2, 3, 64, 64, device=cuda).to(torch.bfloat16))
+    out = m(x)
+    names, seen, stack = set(), set(), [out.grad_fn]
+    while stack:
+        f = stack.pop()
+        if f is None or f in seen:
+            continue
+        seen.add(f)
+        names.add(type(f).__name__)
+        stack.extend(nf for nf, _ in f.next_functions)
+    assert any("Conv3x3" in n for n in names), names
