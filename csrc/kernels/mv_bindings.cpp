@@ -967,6 +967,41 @@ at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at:
   return y;
 }
 
+// data gradient of a stride-1 3x3 conv (dy . flipped filter) with the mode-1 (BN+ReLU)
+// backward reduce of the BN that produced the conv's input fused into the epilogue:
+// returns (d = relu'(x_bn) * dgrad, partials [P, 2, C])
+std::vector<at::Tensor> conv3x3_bn_bwd(at::Tensor dy, at::Tensor wt, at::Tensor x_bn,
+                                       at::Tensor vec) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_bn_bwd: dy must be a channels_last bf16 GPU tensor");
+  TORCH_CHECK(wt.is_cuda() && wt.scalar_type() == at::kBFloat16 && wt.dim() == 4 &&
+                  wt.size(2) == 3 && wt.size(3) == 3 && wt.size(1) == dy.size(1) &&
+                  wt.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_bn_bwd: wt must be the channels_last [C, K, 3, 3] transposed filter");
+  const int64_t N = dy.size(0), K = dy.size(1), H = dy.size(2), W = dy.size(3), C = wt.size(0);
+  TORCH_CHECK(C % 64 == 0 && K % 64 == 0, "conv3x3_bn_bwd: channels must be multiples of 64");
+  TORCH_CHECK(x_bn.is_cuda() && x_bn.scalar_type() == at::kBFloat16 &&
+                  x_bn.sizes() == at::IntArrayRef({N, C, H, W}) &&
+                  x_bn.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_bn_bwd: x_bn must be the BN input [N, C, H, W], channels_last bf16");
+  TORCH_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() &&
+                  vec.numel() == 4 * C, "conv3x3_bn_bwd: saved stats must be fp32 [4, C]");
+  for (const at::Tensor* t : {&wt, &x_bn, &vec})
+    TORCH_CHECK(t->device() == dy.device(), "conv3x3_bn_bwd: devices differ");
+  TORCH_CHECK(N * H * W * std::max(C, K) < (int64_t(1) << 40) && H < 65536 && W < 65536,
+              "conv3x3_bn_bwd: too large");
+  c10::DeviceGuard guard(dy.device());
+  const int64_t M = N * H * W;
+  at::Tensor d = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  at::Tensor part = at::empty({conv3x3_partials(M, C), 2, C}, dy.options().dtype(at::kFloat));
+  TORCH_CHECK(mv_conv3x3(dy.data_ptr(), wt.data_ptr(), d.data_ptr(), (int)N, (int)H, (int)W, (int)K,
+                         (int)C, 1, nullptr, part.data_ptr<float>(), cur_stream(), x_bn.data_ptr(),
+                         vec.data_ptr<float>()),
+              "conv3x3_bn_bwd: unsupported shape");
+  return {d, part};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -1021,6 +1056,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("conv3x3", &conv3x3, "implicit-GEMM 3x3 conv (pad 1) with optional fused BN statistics",
         py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("shift") = py::none(),
         py::arg("partial") = py::none());
+  m.def("conv3x3_bn_bwd", &conv3x3_bn_bwd,
+        "stride-1 3x3 data gradient with the producing BN+ReLU's backward reduce fused");
   m.def("conv3x3_partials", &conv3x3_partials, "partial rows of conv3x3's statistics epilogue");
   m.def("gemm_partials", &gemm_partials, "row tiles (statistics partial rows) of gemm_nt");
 }

@@ -9,5 +9,9 @@ int64_t mv_conv3x3_partials(int64_t M, int K);
 // y[N, Ho, Wo, K] = conv3x3(x[N, H, W, C], w[K, 3, 3, C]); C, K multiples of 64.
 // partial != null: BN statistics of the bf16 outputs around shift (may be null = 0).
 // Returns false for an unsupported shape (nothing launched).
+// bn_x != null (requires partial): the epilogue instead runs the mode-1 (BN+ReLU)
+// backward reduce of the BN whose output x is (y = its data gradient): bn_x = that BN's
+// input [.., K], bn_vec = its saved [4][K] (mean, invstd, scale, bias).
 bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int C, int K,
-                int stride, const float* shift, float* partial, hipStream_t st);
+                int stride, const float* shift, float* partial, hipStream_t st,
+                const void* bn_x = nullptr, const float* bn_vec = nullptr);

@@ -109,10 +109,16 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN, int WM, int WN, bool STATS>
+// EPI: 0 plain, 1 + BN statistics of y (forward), 2 the BN+ReLU (mode 1) backward reduce
+// of the BN whose output was this conv's input: y is the data gradient dy of that output,
+// d = (x_bn * scale + bias > 0) ? bf16(dy) : 0 is written instead, partials (sum d,
+// sum d (x_bn - mean)) — mv_bn.hip's bwd_reduce_kernel<1> folded into the epilogue.
+template <int BM, int BN, int WM, int WN, int EPI>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Wt, __bf16* __restrict__ Y, Geo g,
-    int ntn, int64_t ntm, const float* __restrict__ shift, float* __restrict__ partial) {
+    int ntn, int64_t ntm, const float* __restrict__ shift, float* __restrict__ partial,
+    const __bf16* __restrict__ bnx, const float* __restrict__ bnvec) {
+  constexpr bool STATS = EPI != 0;
   constexpr int NT = WM * WN * 64;
   constexpr int A_CH = BM * 8 / NT;               // 16-byte chunks per thread per A stage
   constexpr int WTN = BN / WN, WTM = BM / WM;
@@ -158,12 +164,18 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
 
   const int gq = lane >> 4, rl = lane & 15;
   float sh[TN][4], s1[TN][4], s2[TN][4];
+  float bsc[EPI == 2 ? TN : 1][4], bbi[EPI == 2 ? TN : 1][4];
 #pragma unroll
   for (int a = 0; a < TN; ++a)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int col = n0 + wn * WTN + a * 16 + 4 * gq + r;
-      sh[a][r] = (STATS && shift) ? shift[col] : 0.f;
+      sh[a][r] = (EPI == 1 && shift) ? shift[col] : 0.f;
+      if constexpr (EPI == 2) {
+        sh[a][r] = bnvec[col];                   // saved mean
+        bsc[a][r] = bnvec[2 * g.K + col];        // scale = gamma * invstd
+        bbi[a][r] = bnvec[3 * g.K + col];        // bias = beta - mean * scale
+      }
       s1[a][r] = 0.f;
       s2[a][r] = 0.f;
     }
@@ -239,9 +251,26 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
           for (int a = 0; a < TN; ++a) {
             const f32x4v v = acc[a][b];
             const int col = n0 + wn * WTN + a * 16 + 4 * gq;
-            *reinterpret_cast<u32x2*>(Y + row * g.K + col) =
-                u32x2{cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3])};
-            if (STATS) {
+            if constexpr (EPI == 2) {
+              const u32x2 xw = *reinterpret_cast<const u32x2*>(bnx + row * g.K + col);
+              const float xv[4] = {__uint_as_float(xw[0] << 16), __uint_as_float(xw[0] & 0xffff0000u),
+                                   __uint_as_float(xw[1] << 16), __uint_as_float(xw[1] & 0xffff0000u)};
+              float dv[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float d =
+                    __builtin_fmaf(xv[r], bsc[a][r], bbi[a][r]) > 0.f ? round_bf16(v[r]) : 0.f;
+                dv[r] = d;
+                s1[a][r] += d;
+                s2[a][r] += d * (xv[r] - sh[a][r]);
+              }
+              *reinterpret_cast<u32x2*>(Y + row * g.K + col) =
+                  u32x2{cvt_pk_bf16(dv[0], dv[1]), cvt_pk_bf16(dv[2], dv[3])};
+            } else {
+              *reinterpret_cast<u32x2*>(Y + row * g.K + col) =
+                  u32x2{cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3])};
+            }
+            if (EPI == 1) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float d = round_bf16(v[r]) - sh[a][r];
@@ -304,10 +333,10 @@ struct Cfg<64, STATS> {
   static constexpr int BM = 256, WM = 4, WN = 2;
 };
 
-template <int BN, bool STATS>
+template <int BN, bool STATS, int EPI = STATS ? 1 : 0>
 static const void* kernel_ptr() {
   using C = Cfg<BN, STATS>;
-  return (const void*)&conv3x3_kernel<C::BM, BN, C::WM, C::WN, STATS>;
+  return (const void*)&conv3x3_kernel<C::BM, BN, C::WM, C::WN, EPI>;
 }
 
 template <int BN, bool STATS>
@@ -347,7 +376,8 @@ int64_t mv_conv3x3_partials(int64_t M, int K) {
 }
 
 bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int C, int K,
-                int stride, const float* shift, float* partial, hipStream_t st) {
+                int stride, const float* shift, float* partial, hipStream_t st,
+                const void* bn_x, const float* bn_vec) {
   using namespace mv::conv;
   if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2)) return false;
   Geo g;
@@ -362,15 +392,22 @@ bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int 
   const __bf16* X = (const __bf16*)x;
   const __bf16* Wt = (const __bf16*)w;
   __bf16* Y = (__bf16*)y;
+  const __bf16* BX = (const __bf16*)bn_x;
+  if (bn_x && !partial) return false;
 #define MV_LAUNCH(BNV, ST)                                                                     \
   {                                                                                            \
     constexpr int BMV = Cfg<BNV, ST>::BM, WMV = Cfg<BNV, ST>::WM, WNV = Cfg<BNV, ST>::WN;      \
     const int64_t ntm = (g.M + BMV - 1) / BMV;                                                 \
     const int ntn = K / BNV;                                                                   \
     const int64_t ns = streams_for<BNV, ST>(ntm, ntn);                                         \
-    hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, WNV, ST>), dim3((unsigned)(ns * ntn)),      \
-                       dim3(WMV * WNV * 64),                                                   \
-                       0, st, X, Wt, Y, g, ntn, ntm, shift, partial);                         \
+    if (BX)                                                                                    \
+      hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, WNV, 2>), dim3((unsigned)(ns * ntn)),     \
+                         dim3(WMV * WNV * 64), 0, st, X, Wt, Y, g, ntn, ntm, shift, partial, BX, \
+                         bn_vec);                                                              \
+    else                                                                                       \
+      hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, WNV, ST ? 1 : 0>),                       \
+                         dim3((unsigned)(ns * ntn)), dim3(WMV * WNV * 64), 0, st, X, Wt, Y, g,   \
+                         ntn, ntm, shift, partial, BX, bn_vec);                                \
   }
   if (conv_bn_of(K) == 128) {
     if (partial) MV_LAUNCH(128, true) else MV_LAUNCH(128, false)

@@ -47,15 +47,17 @@ class GradSlot:
     (1 extra read).  Autograd still orders the producer after the tap: a None
     gradient satisfies the dependency edge.
     """
-    __slots__ = ("grad", "stride", "full_shape", "bn", "pending")
+    __slots__ = ("grad", "stride", "full_shape", "bn", "mode", "pending")
 
     def __init__(self):
         self.grad = None
         self.stride = 1          # > 1: grad is on the stride-s grid (downsample_tap)
         self.full_shape = None   # the tapped output's shape when stride > 1
-        # (x, mask, vec) of the producing mode-3 BN, for a consumer conv whose data
-        # gradient GEMM runs this BN's backward reduce (ops.conv._Conv1x1BN) ...
+        # (x, mask, vec) of the producing BN (mode 3: add+ReLU with its bitmask; mode 1:
+        # ReLU, mask None), for a consumer conv whose data-gradient kernel runs this BN's
+        # backward reduce (ops.conv._Conv1x1BN / _Conv3x3) ...
         self.bn = None
+        self.mode = 0
         # ... and its result (dz, partials), consumed by the BN backward
         self.pending = None
 
@@ -178,8 +180,9 @@ class _BNActTrain(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.slot = slot
         ctx.save_for_backward(x, keep, vec, weight)
-        if slot is not None and mode == 3:
+        if slot is not None and mode in (1, 3):
             slot.bn = (x, keep, vec)
+            slot.mode = mode
             ctx.set_materialize_grads(False)    # dy is None when a consumer took the reduce
         return y
 
@@ -198,9 +201,12 @@ class _BNActTrain(torch.autograd.Function):
             assert ctx.slot.grad is None, "a tapped output has one shortcut consumer"
             if dy is None:
                 dx, dg, db = K.native().bn_bwd_from_partials(dz, x, vec, weight, need_affine, part)
-            else:   # a further consumer: d = mask ? dy + dz : 0 (dz is already masked)
+            elif ctx.mode == 3:   # a further consumer: d = mask ? dy + dz : 0 (dz is masked)
                 dx, dg, db, dz = K.native().bn_bwd(3, _cl(dy), x, y, vec, weight, need_affine,
                                                    dz, 1)
+            else:                 # mode 1: relu'(x) (dy + dz) = relu'(x) dy + dz
+                dx, dg, db, _ = K.native().bn_bwd(1, _cl(dy) + dz, x, None, vec, weight,
+                                                  need_affine, None, 1)
             return (dx if ctx.needs_input_grad[0] else None,
                     dg if ctx.needs_input_grad[1] else None,
                     db if ctx.needs_input_grad[2] else None,
@@ -232,7 +238,8 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentu
         if residual is not None:
             residual = _cl(residual)
         if training:
-            slot = GradSlot() if (relu and residual is not None) else None
+            # mode 2/3: shortcut-gradient taps + fused consumer reduce; mode 1: fused reduce
+            slot = GradSlot() if relu else None
             y = _BNActTrain.apply(x, weight, bias, running_mean, running_var, float(momentum),
                                   float(eps), bool(relu), residual, slot, stats)
             if slot is not None:
@@ -395,11 +402,13 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = Fa
     the BN is training with running statistics, and with x's producer BN backward
     reduce run in this conv's data-gradient GEMM when x is a fused BN+add+ReLU output
     (ops.conv.bwd_fusable); the plain composition otherwise."""
-    from .conv import bwd_fusable, conv1x1_bn, conv3x3_bn, conv3x3_eligible, stats_fusable
+    from .conv import (bwd3x3_fusable, bwd_fusable, conv1x1_bn, conv3x3_bn, conv3x3_eligible,
+                       stats_fusable)
     train_stats = (bn.training and bn.track_running_stats and bn.running_mean is not None
                    and _fusable(x, bn.weight))
     if conv3x3_eligible(conv, x):
-        y, part = conv3x3_bn(conv, x, bn.running_mean if train_stats else None, train_stats)
+        y, part = conv3x3_bn(conv, x, bn.running_mean if train_stats else None, train_stats,
+                             bwd3x3_fusable(conv, x))
         return bn(y, residual=residual, relu=relu, stats=part if train_stats else None)
     fwd = train_stats and stats_fusable(conv, x)
     slot = bwd_fusable(conv, x)

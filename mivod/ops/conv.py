@@ -158,7 +158,7 @@ def bwd_fusable(m: nn.Conv2d, x: torch.Tensor):
     """GradSlot of x's producer when this 1x1 conv's data gradient can carry that
     producer's BN backward reduce (Cout = the GEMM's K in {64, 128, 256}); else None."""
     slot = getattr(x, "_mv_slot", None)
-    if (slot is None or getattr(slot, "bn", None) is None
+    if (slot is None or getattr(slot, "bn", None) is None or getattr(slot, "mode", 0) != 3
             or os.environ.get("MIVOD_CONV_BN_BWD_FUSE", "1") == "0"
             or not (torch.is_grad_enabled() and x.requires_grad) or not _eligible(m, x)
             or tuple(m.kernel_size) != (1, 1) or m.out_channels not in (64, 128, 256)
@@ -202,11 +202,14 @@ class _Conv3x3(torch.autograd.Function):
     mv_conv.hip), optionally with the following BatchNorm's statistics partials of y
     around ``shift`` (non-differentiable second output).  Backward: stride-1 data
     gradient as a forward conv with the flipped, channel-transposed filter (mivod's
-    kernel for <= 128 channels, MIOpen's forward solver otherwise), stride-2 data
-    gradient and the weight gradient from MIOpen."""
+    kernel for <= 128 channels, MIOpen's forward solver otherwise) — and when x is the
+    output of a fused BN+ReLU (``slot``, mode 1), mivod's kernel also runs that BN's
+    backward reduce in its epilogue and hands (d, partials) to it through the slot, the
+    same protocol as ``_Conv1x1BN``; stride-2 data gradient and the weight gradient
+    from MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, shift, stats):
+    def forward(ctx, x, w, stride, shift, stats, slot):
         from . import kernels as K
         nat = K.native()
         wc = w.contiguous(memory_format=torch.channels_last)
@@ -222,6 +225,7 @@ class _Conv3x3(torch.autograd.Function):
             y = nat.conv3x3(x, wc, stride)
         ctx.save_for_backward(x, w)
         ctx.stride = stride
+        ctx.slot = slot
         ctx.mark_non_differentiable(part)
         return y, part
 
@@ -230,6 +234,7 @@ class _Conv3x3(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         s = ctx.stride
+        slot, ctx.slot = ctx.slot, None
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dx = dw = None
         if s == 1:
@@ -237,7 +242,13 @@ class _Conv3x3(torch.autograd.Function):
                 wt = _transposed_filter(w)
                 if _dgrad_on_mivod(w.shape[1], w.shape[0]):
                     from . import kernels as K
-                    dx = K.native().conv3x3(dy, wt, 1)
+                    if (slot is not None and slot.bn is not None and slot.mode == 1
+                            and slot.pending is None):
+                        xb, _, vec = slot.bn
+                        d, part = K.native().conv3x3_bn_bwd(dy, wt, xb, vec)
+                        slot.pending = (d, part)
+                    else:
+                        dx = K.native().conv3x3(dy, wt, 1)
                 else:
                     dx = F.conv2d(dy, wt, None, 1, 1)
             if need_w:
@@ -246,12 +257,24 @@ class _Conv3x3(torch.autograd.Function):
         else:
             dx, dw, _ = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [need_x, need_w, False])
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
-def conv3x3_bn(m: nn.Conv2d, x: torch.Tensor, shift, stats: bool):
+def bwd3x3_fusable(m: nn.Conv2d, x: torch.Tensor):
+    """GradSlot of x's producer when this stride-1 3x3 conv's data gradient runs on
+    mivod's kernel and can carry that producer's BN+ReLU backward reduce; else None."""
+    slot = getattr(x, "_mv_slot", None)
+    if (slot is None or getattr(slot, "bn", None) is None or getattr(slot, "mode", 0) != 1
+            or os.environ.get("MIVOD_CONV_BN_BWD_FUSE", "1") == "0"
+            or not (torch.is_grad_enabled() and x.requires_grad) or m.stride[0] != 1
+            or not _dgrad_on_mivod(m.in_channels, m.out_channels)):
+        return None
+    return slot
+
+
+def conv3x3_bn(m: nn.Conv2d, x: torch.Tensor, shift, stats: bool, slot=None):
     """(y, partial) — see _Conv3x3; ``shift`` is the BN's running mean (stats only)."""
-    return _Conv3x3.apply(x, m.weight, int(m.stride[0]), shift, stats)
+    return _Conv3x3.apply(x, m.weight, int(m.stride[0]), shift, stats, slot)
 
 
 class Conv2d(nn.Conv2d):

@@ -103,3 +103,45 @@ def test_resnet_bottleneck_uses_conv3x3(cuda):
         names.add(type(f).__name__)
         stack.extend(nf for nf, _ in f.next_functions)
     assert any("Conv3x3" in n for n in names), names
+
+
+@pytest.mark.parametrize("c,k", [(64, 64), (128, 128), (64, 128)])
+def test_conv3x3_bn_bwd_matches_reference(cuda, c, k):
+    """dgrad (forward conv with the transposed filter) + mode-1 BN backward reduce in
+    the epilogue == conv2d + relu mask + (sum d, sum d (x - mean)) in fp32."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(c + 7 * k)
+    n, h, w = 3, 11, 9
+    dy = _cl(torch.randn(n, k, h, w, device=cuda, generator=g).to(torch.bfloat16))
+    wt = _cl((torch.randn(c, k, 3, 3, device=cuda, generator=g) / (9 * k) ** 0.5).to(torch.bfloat16))
+    xb = _cl(torch.randn(n, c, h, w, device=cuda, generator=g).to(torch.bfloat16))
+    vec = torch.randn(4, c, device=cuda, generator=g)
+    d, part = nat.conv3x3_bn_bwd(dy, wt, xb, vec)
+    dg = F.conv2d(dy.float(), wt.float(), None, 1, 1).to(torch.bfloat16).float()
+    on = (xb.float() * vec[2].view(1, -1, 1, 1) + vec[3].view(1, -1, 1, 1)) > 0
+    ref = torch.where(on, dg, torch.zeros_like(dg))
+    torch.testing.assert_close(d.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
+    rr = ref.permute(0, 2, 3, 1).reshape(-1, c)
+    xr = xb.float().permute(0, 2, 3, 1).reshape(-1, c)
+    sm = part.sum(0)
+    torch.testing.assert_close(sm[0], rr.sum(0), rtol=2e-2, atol=0.5)
+    torch.testing.assert_close(sm[1], (rr * (xr - vec[0])).sum(0), rtol=2e-2, atol=1.0)
+
+
+def test_resnet_uses_conv3x3_bwd_fusion(cuda, monkeypatch):
+    """conv2's data gradient carries BN1's backward reduce on the <=128-channel layers."""
+    from mivod.models.resnet import ResNet, to_mixed_bf16
+    nat = _nat()
+    calls = []
+    real = nat.conv3x3_bn_bwd
+
+    def counted(*a):
+        calls.append(a[0].shape)
+        return real(*a)
+
+    monkeypatch.setattr(nat, "conv3x3_bn_bwd", counted)
+    torch.manual_seed(0)
+    m = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
+    x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
+    F.cross_entropy(m(x).float(), torch.randint(0, 10, (4,), device=cuda)).backward()
+    assert len(calls) == 3, calls       # layer1.0, layer1.1, layer2.1 (layer2.0 is strided)
