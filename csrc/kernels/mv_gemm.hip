@@ -257,12 +257,11 @@ __device__ __forceinline__ void ld_raw(const __bf16* p, uint32_t (&r)[NC / 2]) {
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-template <int K, int BN, int EPI>
+template <int K, int BN, int EPI, int BM = 64>
 __global__ __launch_bounds__(256) void gemm_stream_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
     int64_t M, int N, int ntn, int64_t ntm, const float* __restrict__ shift,
     float* __restrict__ partial, BwdEpi be) {
-  constexpr int BM = 64;
   constexpr int KCH = K / 8;                 // 16-byte chunks per row
   constexpr int A_CH = BM * KCH / 256;       // A chunks per thread per tile
   constexpr int W_CH = BN * KCH / 256;
@@ -485,18 +484,25 @@ static bool stream_cfg(int K, int N, int* bn) {
   return false;
 }
 
+// rows per streamed tile: the K = 256 backward-reduce variant streams 32-row tiles so two
+// workgroups fit a CU (its 64 KB filter slice + 16 KB A tile) — its epilogue reads three
+// [M, N] operands, so resident waves matter more than MFMA tile depth
+template <int K, int EPI>
+constexpr int stream_bm() { return (K == 256 && EPI == 2) ? 32 : 64; }
+
 template <int K, int BN, int EPI>
 static int64_t streams_for(int64_t M, int N) {
+  constexpr int BMV = stream_bm<K, EPI>();
   static int per = [] {
     int v = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &v, (const void*)&mv::gemm::gemm_stream_kernel<K, BN, EPI>, 256, 0) != hipSuccess ||
+            &v, (const void*)&mv::gemm::gemm_stream_kernel<K, BN, EPI, BMV>, 256, 0) != hipSuccess ||
         v < 1)
       v = 1;
     return v;
   }();
   const int ntn = N / BN;
-  const int64_t ntm = (M + 63) / 64;
+  const int64_t ntm = (M + BMV - 1) / BMV;
   int64_t streams = (int64_t)num_cus() * per / ntn;
   if (streams < 1) streams = 1;
   if (streams > ntm) streams = ntm;
@@ -509,18 +515,21 @@ static void launch_stream(const __bf16* a, const __bf16* b, __bf16* c, int64_t M
                           hipStream_t st) {
   using namespace mv::gemm;
   const int ntn = N / BN;
-  const int64_t ntm = (M + 63) / 64;
   BwdEpi e{};
   if (be) {
     e = *be;
+    constexpr int BMV = stream_bm<K, 2>();
+    const int64_t ntm = (M + BMV - 1) / BMV;
     const dim3 grid((unsigned)(streams_for<K, BN, 2>(M, N) * ntn));
-    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 2>), grid, dim3(256), 0, st, a, b, c, M, N,
+    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 2, BMV>), grid, dim3(256), 0, st, a, b, c, M, N,
                        ntn, ntm, shift, partial, e);
   } else if (partial) {
+    const int64_t ntm = (M + 63) / 64;
     const dim3 grid((unsigned)(streams_for<K, BN, 1>(M, N) * ntn));
     hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 1>), grid, dim3(256), 0, st, a, b, c, M, N,
                        ntn, ntm, shift, partial, e);
   } else {
+    const int64_t ntm = (M + 63) / 64;
     const dim3 grid((unsigned)(streams_for<K, BN, 0>(M, N) * ntn));
     hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 0>), grid, dim3(256), 0, st, a, b, c, M, N,
                        ntn, ntm, shift, partial, e);
