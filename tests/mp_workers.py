@@ -961,6 +961,21 @@ def gpu_rccl_single():
         torch.testing.assert_close(p.detach(), q - 0.1 * gr, rtol=1e-5, atol=1e-6)
     calls = C.gpu_stats()["calls"] - calls0
     assert calls >= 14, calls
+    # the hierarchical branch (reduce-scatter / cross allreduce / allgather on
+    # ncclCommSplit children) with 1-rank local and cross comms
+    st.gpu_local = st.gpu.split(0, 0)
+    st.gpu_cross = st.gpu.split(0, 0)
+    assert st.gpu_local.size == 1 and st.gpu_cross.size == 1
+    for n in (1000, 4097):
+        h = torch.arange(n, device=dev, dtype=torch.float32) % 13
+        ref = h.clone()
+        C._hierarchical_gpu_(h, C.Sum, 0.5)
+        torch.testing.assert_close(h, ref * 0.5)
+        C._hierarchical_gpu_(h, C.Average, 1.0)
+        torch.testing.assert_close(h, ref * 0.5)
+    st.gpu_local.close()
+    st.gpu_cross.close()
+    st.gpu_local = st.gpu_cross = None
     st.gpu.check()
     hvd.shutdown()
     print("OK", 0)
