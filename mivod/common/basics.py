@@ -200,7 +200,9 @@ def init(comm=None, process_sets=None):
             _state.backend = "local"
             if use_gpu and os.environ.get("MIVOD_FORCE_COLLECTIVES", "0") == "1":
                 from ..parallel.transport import RcclTransport
-                _state.gpu = RcclTransport.create(0, 1, _state.device)
+                _state.gpu = RcclTransport.create(
+                    0, 1, _state.device,
+                    timeout_s=float(os.environ.get("MIVOD_RCCL_TIMEOUT_S", "0") or 0))
                 _state.backend = "rccl"
         ORDER.reset(enabled=_state.gpu is not None and _state.size > 1)
         _state.initialized = True

@@ -1120,5 +1120,39 @@ def keras_static():
     print("OK", r)
 
 
+def gpu_rccl_watchdog():
+    """The communicator watchdog: a collective that cannot complete within
+    MIVOD_RCCL_TIMEOUT_S (here: queued behind a ~3 s spin kernel) makes the watchdog
+    thread abort the communicator (ncclCommAbort); the next collective raises."""
+    import time as _t
+
+    from mivod.common import basics as B
+    from mivod.parallel import collectives as C
+    hvd.init()
+    st = B.state()
+    assert st.gpu is not None and st.gpu.name == "rccl"
+    dev = hvd.device()
+    x = torch.ones(4096, device=dev)
+    torch.cuda._sleep(int(6e9))            # bounded spin on the current stream
+    C.allreduce_(x, C.Sum)                 # its completion event is stuck behind the spin
+    t0, err = _t.time(), ""
+    while _t.time() - t0 < 30:
+        err = st.gpu.comm.error()
+        if err:
+            break
+        _t.sleep(0.1)
+    assert "did not complete" in err, err
+    try:
+        C.allreduce_(x, C.Sum)
+    except RuntimeError as e:
+        assert "aborted" in str(e), e
+    else:
+        raise AssertionError("a collective on an aborted communicator did not raise")
+    torch.cuda.synchronize()
+    print("OK", 0, flush=True)
+    os._exit(0)      # the aborted communicator is not destroyed again at exit
+
+
+
 if __name__ == "__main__":
     globals()[sys.argv[1]]()

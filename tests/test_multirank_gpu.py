@@ -32,6 +32,14 @@ def test_gpu_rccl_communicator_world1(cuda):
               extra_env={"MIVOD_TRANSPORT": "rccl", "MIVOD_FORCE_COLLECTIVES": "1"})
 
 
+def test_gpu_rccl_watchdog_aborts_a_stuck_collective(cuda):
+    """Failure detection on hardware: the RCCL watchdog (csrc/comm/comm.cc) aborts a
+    communicator whose collective outlives MIVOD_RCCL_TIMEOUT_S and later calls raise."""
+    run_ranks("gpu_rccl_watchdog", 1, timeout=120,
+              extra_env={"MIVOD_TRANSPORT": "rccl", "MIVOD_FORCE_COLLECTIVES": "1",
+                         "MIVOD_RCCL_TIMEOUT_S": "1"})
+
+
 def test_gpu_xgmi_mesh_one_shot_allreduce(cuda):
     """K7: the HIP-IPC mesh allreduce kernel between two processes on one GPU."""
     run_ranks("gpu_mesh", 2, timeout=180,
