@@ -21,6 +21,8 @@
 #include "mv_bert.h"
 #include "mv_common.h"
 
+#include <cstdlib>
+
 namespace mv {
 namespace tx {
 
@@ -40,9 +42,32 @@ __device__ __forceinline__ bool keep(uint32_t seed, uint32_t row, uint32_t col, 
   return mix32(mix32(seed + row * 0x9E3779B1u) + col * 0x85EBCA6Bu) >= th;
 }
 
-__device__ __forceinline__ float gelu(float v) { return 0.5f * v * (1.f + erff(v * kSqrt1_2)); }
+// Exact-erf GELU (BERT's), with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7,
+// far below bf16's 4e-3 resolution): one reciprocal, a 5-term polynomial and ONE
+// exponential, exp(-v^2 / 2), which gelu'(v) reuses for the Gaussian pdf term.  ocml's
+// erff is a branchy piecewise rational approximation; with it the bias-GELU passes were
+// VALU-bound at ~2.4 TB/s (profiles/r2_bert_large_bs512_short_attn_bwd.md).
+__device__ __forceinline__ void gelu_parts(float v, float* cdf, float* e) {
+  const float z = fabsf(v) * kSqrt1_2;
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f, z, 1.f));
+  float p = __builtin_fmaf(1.061405429f, t, -1.453152027f);
+  p = __builtin_fmaf(p, t, 1.421413741f);
+  p = __builtin_fmaf(p, t, -0.284496736f);
+  p = __builtin_fmaf(p, t, 0.254829592f);
+  p *= t;
+  *e = __expf(-z * z);                               // exp(-v^2 / 2)
+  const float erf_abs = __builtin_fmaf(-p, *e, 1.f);
+  *cdf = 0.5f + 0.5f * __builtin_copysignf(erf_abs, v);
+}
+__device__ __forceinline__ float gelu(float v) {
+  float cdf, e;
+  gelu_parts(v, &cdf, &e);
+  return v * cdf;
+}
 __device__ __forceinline__ float gelu_grad(float v) {
-  return 0.5f * (1.f + erff(v * kSqrt1_2)) + v * kInvSqrt2Pi * __expf(-0.5f * v * v);
+  float cdf, e;
+  gelu_parts(v, &cdf, &e);
+  return __builtin_fmaf(v * kInvSqrt2Pi, e, cdf);
 }
 
 // --------------------------------------------------------------- bias + GELU
@@ -283,17 +308,51 @@ __device__ __forceinline__ void block_colsum(const float (&src)[NCH][8], float (
 
 template <int NCH>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float inv_keep = a.p_drop > 0.f ? 1.f / (1.f - a.p_drop) : 1.f;
-  float dg[NCH][8], db[NCH][8], dzs[NCH][8];
+  float dg[NCH][8], db[NCH][8], dzs[NCH][8], gm[NCH][8];
 #pragma unroll
-  for (int k = 0; k < NCH; ++k)
+  for (int k = 0; k < NCH; ++k) {
+    const int c = k * 512 + lane * 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dg[k][j] = db[k][j] = dzs[k][j] = 0.f;
+    for (int j = 0; j < 8; ++j) dg[k][j] = db[k][j] = dzs[k][j] = gm[k][j] = 0.f;
+    if (c < a.H) load8(a.gamma + c, gm[k]);       // once per kernel, not per row
+  }
+  // the next row's dy / dy2 / v are loaded (raw 16-byte vectors) while the current
+  // row is reduced and written: a wave keeps two rows of loads in flight instead of
+  // waiting a full memory latency at the top of every row
+  struct Raw {
+    u32x4 dy[NCH], d2[NCH], v[NCH];
+  };
+  auto ld = [&](int64_t row, Raw& R) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = k * 512 + lane * 8;
+      R.dy[k] = R.d2[k] = R.v[k] = u32x4{0u, 0u, 0u, 0u};
+      if (c < a.H && row < a.M) {
+        R.dy[k] = *reinterpret_cast<const u32x4*>(a.dy + row * a.H + c);
+        if (a.dy2) R.d2[k] = *reinterpret_cast<const u32x4*>(a.dy2 + row * a.H + c);
+        R.v[k] = *reinterpret_cast<const u32x4*>(a.v + row * a.H + c);
+      }
+    }
+  };
+  auto unpack = [](const u32x4& r, float (&o)[8]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[2 * j] = __uint_as_float(r[j] << 16);
+      o[2 * j + 1] = __uint_as_float(r[j] & 0xffff0000u);
+    }
+  };
   const int64_t rbeg = (int64_t)blockIdx.x * kRowsPerBlock + w * (kRowsPerBlock / 4);
+  constexpr bool PF = NCH <= 2;         // wider rows: no room for a second row of loads
+  Raw cur, nxt;
+  if (PF) ld(rbeg, cur);
   for (int rr = 0; rr < kRowsPerBlock / 4; ++rr) {
     const int64_t row = rbeg + rr;
     if (row >= a.M) break;
+    if (!PF) ld(row, cur);
+    else if (rr + 1 < kRowsPerBlock / 4) ld(row + 1, nxt);
     const float mean = a.mean[row], rstd = a.rstd[row];
     float xh[NCH][8], g[NCH][8];
     float s1 = 0.f, s2 = 0.f;
@@ -303,20 +362,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) xh[k][j] = g[k][j] = 0.f;
       if (c < a.H) {
-        float dy[8], vv[8], gm[8];
-        load8(a.dy + row * a.H + c, dy);
+        float dy[8], vv[8];
+        unpack(cur.dy[k], dy);
         if (a.dy2) {   // residual use of y (mivod.ops.bn.tap): no separate autograd add
           float e[8];
-          load8(a.dy2 + row * a.H + c, e);
+          unpack(cur.d2[k], e);
 #pragma unroll
           for (int j = 0; j < 8; ++j) dy[j] += e[j];
         }
-        load8(a.v + row * a.H + c, vv);
-        load8(a.gamma + c, gm);
+        unpack(cur.v[k], vv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[k][j] = (vv[j] - mean) * rstd;
-          g[k][j] = dy[j] * gm[j];
+          g[k][j] = dy[j] * gm[k][j];
           s1 += g[k][j];
           s2 += g[k][j] * xh[k][j];
           dg[k][j] += dy[j] * xh[k][j];
@@ -344,6 +402,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwdArgs a) {
         if (a.dz) store8(a.dz + row * a.H + c, z);
       }
     }
+    if (PF) cur = nxt;
   }
   __shared__ float red[4][512];
   float* base = a.partial + (int64_t)blockIdx.x * 3 * a.H;
@@ -359,7 +418,12 @@ using namespace mv::tx;
 
 static int64_t rows_per_block_for(int64_t M, int N, int64_t* P) {
   const int gy = (N + 2047) / 2048;
-  int64_t blocks = 1024 / gy;
+  static const int64_t total = [] {      // workgroups per pass (A/B knob MIVOD_TX_BLOCKS)
+    const char* e = std::getenv("MIVOD_TX_BLOCKS");
+    const int64_t v = e ? std::atoll(e) : 0;
+    return v > 0 ? v : (int64_t)1024;
+  }();
+  int64_t blocks = total / gy;
   if (blocks < 1) blocks = 1;
   int64_t rpb = (M + blocks - 1) / blocks;
   if (rpb < 8) rpb = 8;
