@@ -6,6 +6,10 @@
 // v_mfma_f32_16x16x32_bf16 (wave64; lane l holds A[l&15][8(l>>4)+j],
 // B[8(l>>4)+j][l&15], C/D row (l>>4)*4+r, col l&15).
 //
+// The k-major operands (V^T, Q^T, dO^T, K^T) are read from row-major LDS images with
+// gfx950's transposed LDS read (ds_read_b64_tr_b16, tr8 below): no element-wise
+// transposed LDS copies.
+//
 // Forward (one workgroup = 4 waves = 64 queries of one (b, h)): each wave keeps
 // its 16 query rows as MFMA B fragments, streams K / V^T blocks of 64 keys
 // through LDS, computes S^T = K Q^T so that every lane owns ONE query column
@@ -77,14 +81,26 @@ __device__ __forceinline__ bf16x8 ld_b128(const __bf16* p) {
   return *reinterpret_cast<const bf16x8*>(p);
 }
 
-// 8 bf16 from two 4-element (8-byte) runs
-__device__ __forceinline__ bf16x8 ld_2x4(const __bf16* p0, const __bf16* p1) {
-  u16x4 a = *reinterpret_cast<const u16x4*>(p0);
-  u16x4 b = *reinterpret_cast<const u16x4*>(p1);
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// gfx950 transposed LDS read (ds_read_b64_tr_b16): each 16-lane group reads a 4-row x
+// 16-column block of a row-major bf16 LDS array and lane c receives column col0 + c of
+// rows r0 .. r0 + 3 — the k-major MFMA operand straight from a row-major image, no
+// transposed copy.  Lane c supplies the address of row r0 + c/4, columns 4(c%4) ...
+__device__ __forceinline__ s16x4 tr4(const __bf16* base, int stride, int r0, int col0, int c) {
+  const __bf16* p = base + (r0 + (c >> 2)) * stride + col0 + 4 * (c & 3);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+}
+
+// 8 k-values: rows ra .. ra+3 then rb .. rb+3 of column col0 + c
+__device__ __forceinline__ bf16x8 tr8(const __bf16* base, int stride, int ra, int rb, int col0,
+                                      int c) {
+  const s16x4 a = tr4(base, stride, ra, col0, c);
+  const s16x4 b = tr4(base, stride, rb, col0, c);
   bf16x8 o;
-  unsigned short* s = reinterpret_cast<unsigned short*>(&o);
-  s[0] = a[0]; s[1] = a[1]; s[2] = a[2]; s[3] = a[3];
-  s[4] = b[0]; s[5] = b[1]; s[6] = b[2]; s[7] = b[3];
+  short* q = reinterpret_cast<short*>(&o);
+  q[0] = a[0]; q[1] = a[1]; q[2] = a[2]; q[3] = a[3];
+  q[4] = b[0]; q[5] = b[1]; q[6] = b[2]; q[7] = b[3];
   return o;
 }
 
@@ -106,7 +122,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(AttnParams p) {
   const __bf16* Kb = Qb + (int64_t)p.h * D;
   const __bf16* Vb = Qb + 2LL * p.h * D;
   __shared__ __attribute__((aligned(16))) __bf16 Ks[KB][D + PAD];
-  __shared__ __attribute__((aligned(16))) __bf16 Vt[D][KB + PAD];
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[KB][D + PAD];   // row-major; V^T via tr8
 
   bf16x8 qf[2];
   {
@@ -135,11 +151,8 @@ __global__ __launch_bounds__(256) void fwd_kernel(AttnParams p) {
       }
       *reinterpret_cast<bf16x8*>(&Ks[key][d0]) = k0;
       *reinterpret_cast<bf16x8*>(&Ks[key][d0 + 8]) = k1;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Vt[d0 + j][key] = v0[j];
-        Vt[d0 + 8 + j][key] = v1[j];
-      }
+      *reinterpret_cast<bf16x8*>(&Vs[key][d0]) = v0;
+      *reinterpret_cast<bf16x8*>(&Vs[key][d0 + 8]) = v1;
     }
     __syncthreads();
     // S^T tiles: st[t][r] = score(key kb0 + 16t + 4g + r, query q0 + c)
@@ -203,7 +216,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(AttnParams p) {
       const bf16x8 af = pack8(a8);
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        const bf16x8 bfr = ld_2x4(&Vt[16 * n + c][16 * t0 + 4 * g], &Vt[16 * n + c][16 * t1 + 4 * g]);
+        const bf16x8 bfr = tr8(&Vs[0][0], D + PAD, 16 * t0 + 4 * g, 16 * t1 + 4 * g, 16 * n, c);
         O[n] = mfma(af, bfr, O[n]);
       }
     }
@@ -272,11 +285,9 @@ __global__ __launch_bounds__(256) void bwd_kernel(AttnParams p, const __bf16* __
   const __bf16* dOb = dout + (int64_t)bi * p.s * otok + (int64_t)hi * D;
 
   __shared__ __attribute__((aligned(16))) __bf16 Qs[QB][D + PAD];
-  __shared__ __attribute__((aligned(16))) __bf16 Qt[D][QB + PAD];
   __shared__ __attribute__((aligned(16))) __bf16 dOs[QB][D + PAD];
-  __shared__ __attribute__((aligned(16))) __bf16 dOt[D][QB + PAD];
   __shared__ __attribute__((aligned(16))) __bf16 dSs[QB][KB + PAD];
-  __shared__ __attribute__((aligned(16))) __bf16 Kt[D][KB + PAD];
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[KB][D + PAD];     // K^T via tr8
   __shared__ float lse_s[QB], del_s[QB];
 
   // this wave's 16 keys as MFMA B fragments (K^T / V^T columns)
@@ -289,7 +300,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(AttnParams p, const __bf16* __
       vf[ks] = key < p.s ? ld_b128(Vb + (int64_t)key * tok + 32 * ks + 8 * g) : zero8();
     }
   }
-  {  // K^T block for dQ = dS K
+  {  // this block's keys, row-major, for dQ = dS K
     const int t = threadIdx.x, key = t >> 2, d0 = (t & 3) * 16;
     const int kg = kb * KB + key;
     bf16x8 a = zero8(), b2 = zero8();
@@ -297,11 +308,8 @@ __global__ __launch_bounds__(256) void bwd_kernel(AttnParams p, const __bf16* __
       a = ld_b128(Kb + (int64_t)kg * tok + d0);
       b2 = ld_b128(Kb + (int64_t)kg * tok + d0 + 8);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      Kt[d0 + j][key] = a[j];
-      Kt[d0 + 8 + j][key] = b2[j];
-    }
+    *reinterpret_cast<bf16x8*>(&Ks[key][d0]) = a;
+    *reinterpret_cast<bf16x8*>(&Ks[key][d0 + 8]) = b2;
   }
   f32x4v dVt[4], dKt[4];
 #pragma unroll
@@ -330,13 +338,6 @@ __global__ __launch_bounds__(256) void bwd_kernel(AttnParams p, const __bf16* __
       *reinterpret_cast<bf16x8*>(&Qs[row][d0 + 8]) = q1v;
       *reinterpret_cast<bf16x8*>(&dOs[row][d0]) = o0;
       *reinterpret_cast<bf16x8*>(&dOs[row][d0 + 8]) = o1;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Qt[d0 + j][row] = q0v[j];
-        Qt[d0 + 8 + j][row] = q1v[j];
-        dOt[d0 + j][row] = o0[j];
-        dOt[d0 + 8 + j][row] = o1[j];
-      }
       if (t < QB) {
         const int qq = qb0 + t;
         lse_s[t] = qq < p.s ? p.lse[(int64_t)bh * p.s + qq] : INFINITY;
@@ -381,8 +382,8 @@ __global__ __launch_bounds__(256) void bwd_kernel(AttnParams p, const __bf16* __
       const int qa = 32 * ch + 4 * g, qbb = 32 * ch + 16 + 4 * g;
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        dVt[n] = mfma(ld_2x4(&dOt[16 * n + c][qa], &dOt[16 * n + c][qbb]), zf, dVt[n]);
-        dKt[n] = mfma(ld_2x4(&Qt[16 * n + c][qa], &Qt[16 * n + c][qbb]), sf, dKt[n]);
+        dVt[n] = mfma(tr8(&dOs[0][0], D + PAD, qa, qbb, 16 * n, c), zf, dVt[n]);
+        dKt[n] = mfma(tr8(&Qs[0][0], D + PAD, qa, qbb, 16 * n, c), sf, dKt[n]);
       }
     }
     __syncthreads();
@@ -395,7 +396,8 @@ __global__ __launch_bounds__(256) void bwd_kernel(AttnParams p, const __bf16* __
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
           acc = mfma(ld_b128(&dSs[16 * qt + c][32 * ks + 8 * g]),
-                     ld_b128(&Kt[16 * n + c][32 * ks + 8 * g]), acc);
+                     tr8(&Ks[0][0], D + PAD, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, 16 * n, c),
+                     acc);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = qb0 + 16 * qt + 4 * g + r;
@@ -446,12 +448,12 @@ __global__ __launch_bounds__(512) void bwd_short_kernel(AttnParams p,
   const __bf16* dOb = dout + (int64_t)bi * p.s * otok + (int64_t)hi * D;
   const __bf16* Ob = out + (int64_t)bi * p.s * otok + (int64_t)hi * D;
 
+  // row-major images only: the k-major operands (Q^T, dO^T, K^T) come from them through
+  // transposed LDS reads (tr8), so no element-wise transposed copies are written
   __shared__ __attribute__((aligned(16))) __bf16 Qs[QB][D + PAD];
-  __shared__ __attribute__((aligned(16))) __bf16 Qt[D][QB + PAD];
   __shared__ __attribute__((aligned(16))) __bf16 dOs[QB][D + PAD];
-  __shared__ __attribute__((aligned(16))) __bf16 dOt[D][QB + PAD];
   __shared__ __attribute__((aligned(16))) __bf16 dSs[QB][SK + PAD];
-  __shared__ __attribute__((aligned(16))) __bf16 Kt[D][SK + PAD];
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[SK][D + PAD];
   __shared__ float lse_s[QB], del_s[QB];
 
   bf16x8 kf[2], vf[2];
@@ -463,18 +465,15 @@ __global__ __launch_bounds__(512) void bwd_short_kernel(AttnParams p,
       vf[ks] = key < p.s ? ld_b128(Vb + (int64_t)key * tok + 32 * ks + 8 * g) : zero8();
     }
   }
-  {  // K^T of all SK keys for dQ = dS K
+  {  // all SK keys, row-major, for dQ = dS K
     const int t = threadIdx.x, key = t >> 2, d0 = (t & 3) * 16;
     bf16x8 a = zero8(), b2 = zero8();
     if (key < p.s) {
       a = ld_b128(Kb + (int64_t)key * tok + d0);
       b2 = ld_b128(Kb + (int64_t)key * tok + d0 + 8);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      Kt[d0 + j][key] = a[j];
-      Kt[d0 + 8 + j][key] = b2[j];
-    }
+    *reinterpret_cast<bf16x8*>(&Ks[key][d0]) = a;
+    *reinterpret_cast<bf16x8*>(&Ks[key][d0 + 8]) = b2;
   }
   f32x4v dVt[4], dKt[4];
 #pragma unroll
@@ -503,13 +502,6 @@ __global__ __launch_bounds__(512) void bwd_short_kernel(AttnParams p,
       *reinterpret_cast<bf16x8*>(&Qs[row][d0 + 8]) = q1v;
       *reinterpret_cast<bf16x8*>(&dOs[row][d0]) = o0;
       *reinterpret_cast<bf16x8*>(&dOs[row][d0 + 8]) = o1;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Qt[d0 + j][row] = q0v[j];
-        Qt[d0 + 8 + j][row] = q1v[j];
-        dOt[d0 + j][row] = o0[j];
-        dOt[d0 + 8 + j][row] = o1[j];
-      }
       if (t < QB) {
         const int qq = qb0 + t;
         lse_s[t] = qq < p.s ? p.lse[(int64_t)bh * p.s + qq] : INFINITY;
@@ -569,8 +561,8 @@ __global__ __launch_bounds__(512) void bwd_short_kernel(AttnParams p,
       const int qa = 32 * ch + 4 * g, qbb = 32 * ch + 16 + 4 * g;
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        dVt[n] = mfma(ld_2x4(&dOt[16 * n + c][qa], &dOt[16 * n + c][qbb]), zf, dVt[n]);
-        dKt[n] = mfma(ld_2x4(&Qt[16 * n + c][qa], &Qt[16 * n + c][qbb]), sf, dKt[n]);
+        dVt[n] = mfma(tr8(&dOs[0][0], D + PAD, qa, qbb, 16 * n, c), zf, dVt[n]);
+        dKt[n] = mfma(tr8(&Qs[0][0], D + PAD, qa, qbb, 16 * n, c), sf, dKt[n]);
       }
     }
     __syncthreads();
@@ -584,7 +576,7 @@ __global__ __launch_bounds__(512) void bwd_short_kernel(AttnParams p,
 #pragma unroll
         for (int ks = 0; ks < SK / 32; ++ks)
           acc = mfma(ld_b128(&dSs[16 * qt + c][32 * ks + 8 * g]),
-                     ld_b128(&Kt[16 * n + c][32 * ks + 8 * g]), acc);
+                     tr8(&Ks[0][0], D + PAD, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, 16 * n, c), acc);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int q = qb0 + 16 * qt + 4 * g + r;
