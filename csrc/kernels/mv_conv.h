@@ -15,3 +15,9 @@ int64_t mv_conv3x3_partials(int64_t M, int K);
 bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int C, int K,
                 int stride, const float* shift, float* partial, hipStream_t st,
                 const void* bn_x = nullptr, const float* bn_vec = nullptr);
+
+// 3x3 weight gradient: dw[K, 3, 3, C] (bf16, channels_last [K, C, 3, 3]) of
+// y = conv3x3(x, w, stride, pad 1) given dy; work: fp32 [mv_wgrad3x3_workspace(M, K, C)]
+int64_t mv_wgrad3x3_workspace(int64_t M, int K, int C);
+bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
+                 int K, int stride, hipStream_t st);

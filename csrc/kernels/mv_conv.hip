@@ -417,3 +417,208 @@ bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int 
 #undef MV_LAUNCH
   return true;
 }
+
+// ===========================================================================
+// 3x3 weight gradient (pad 1, stride 1 / 2):
+//   dW[k][tap][c] = sum_m dy[m][k] . X[pixel(m) + tap][c]   (filter in [K][3][3][C] order)
+// A GEMM with the reduction over the output pixels m (N*Ho*Wo rows): a workgroup owns
+// one 64(k) x 64(c) block for ALL 9 taps (accumulators resident for the whole kernel)
+// and a contiguous range of 32-row m chunks; per chunk it stages the dy tile and the 9
+// tap-shifted X tiles (gathered rows, zero page at the image border) with
+// global_load_lds into a 2-slot ring (two workgroups per CU).  Both MFMA operands
+// are k(=m)-major, so they are read with gfx950's transposed LDS read
+// (ds_read_b64_tr_b16).  Each workgroup writes an fp32 partial [9][64][64] block; a
+// fixed-order reduce kernel sums the m splits and writes the bf16 filter gradient.
+// ===========================================================================
+namespace mv {
+namespace conv {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// [32][64] bf16 stage tiles (128-B rows) with a row-dependent 16-byte-chunk XOR: slot
+// (r, ch) holds chunk ch ^ wswz(r).  A transposed read touches 4 rows per 16-lane group
+// and rows 8 apart in the other group of its 32-lane half; rows 2 apart share a bank
+// window on 128-B rows, so {r, r+2, r+8, r+10} get chunk offsets {0, 2, 4, 6} (XOR by
+// even values keeps a 32-byte column pair together): conflict-free instead of 4-way.
+__device__ __forceinline__ int wswz(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
+
+__device__ __forceinline__ s16x4 tr4(const __bf16* base, int r0, int col0, int c) {
+  const int r = r0 + (c >> 2), e = col0 + 4 * (c & 3);
+  const __bf16* p = base + r * 64 + (((e >> 3) ^ wswz(r)) << 3) + (e & 7);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+}
+// lane c of each 16-lane group: rows ra..ra+3, rb..rb+3 of column col0 + c
+__device__ __forceinline__ bf16x8 tr8(const __bf16* base, int ra, int rb, int col0, int c) {
+  const s16x4 a = tr4(base, ra, col0, c);
+  const s16x4 b = tr4(base, rb, col0, c);
+  bf16x8 o;
+  short* q = reinterpret_cast<short*>(&o);
+  q[0] = a[0]; q[1] = a[1]; q[2] = a[2]; q[3] = a[3];
+  q[4] = b[0]; q[5] = b[1]; q[6] = b[2]; q[7] = b[3];
+  return o;
+}
+
+constexpr int WG_NT = 256;                 // 4 waves, wave w = c tile w, all 4 k tiles
+constexpr int WG_ROWS = 32;                // m rows per stage (one MFMA k step)
+constexpr int WG_TILE = WG_ROWS * 64;      // elements of one [32][64] tile
+constexpr int WG_STAGE = 10 * WG_TILE;     // dy + 9 taps
+constexpr int WG_NS = 2;                   // 80 KB of LDS: two workgroups (8 waves) per CU
+constexpr int WG_LPS = 10 * 256 / WG_NT;   // glds per thread per stage (10)
+
+__global__ __launch_bounds__(WG_NT) void wgrad3x3_kernel(const __bf16* __restrict__ X,
+                                                          const __bf16* __restrict__ DY,
+                                                          float* __restrict__ partial, Geo g,
+                                                          int nkc, int msplit, int64_t nchunks) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[WG_NS * WG_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t = remap(blockIdx.x, gridDim.x);
+  const int kc = t % nkc, ms = t / nkc;
+  const int cblocks = g.C / 64;
+  const int k0 = (kc / cblocks) * 64, c0 = (kc % cblocks) * 64;
+  const int64_t per = (nchunks + msplit - 1) / msplit;
+  const int64_t ch0 = ms * per;
+  const int64_t ch1 = ch0 + per < nchunks ? ch0 + per : nchunks;
+
+  // staging role: row tid >> 3, 16-byte chunk tid & 7 of all 10 tiles of a stage.  The
+  // row's output pixel advances by 32 per stage: (n, ho, wo) is carried incrementally
+  // (no per-stage division)
+  const int srow = tid >> 3, sch = (tid & 7) ^ wswz(tid >> 3);   // swizzled source chunk
+  const uint64_t zaddr = (uint64_t)(g_zero + (tid & 7) * 4);
+  int64_t pm = ch0 * WG_ROWS + srow;           // this thread's row of the next issued stage
+  int pn = 0, pho = 0, pwo = 0;
+  {
+    const int64_t hw = (int64_t)g.Ho * g.Wo;
+    const int64_t mm = pm < g.M ? pm : 0;
+    pn = (int)(mm / hw);
+    const int rem = (int)(mm - (int64_t)pn * hw);
+    pho = rem / g.Wo;
+    pwo = rem - pho * g.Wo;
+  }
+  auto issue = [&](int slot) {
+    const bool in = pm < g.M;
+    const int hi0 = pho * g.st - 1, wi0 = pwo * g.st - 1;
+    const int64_t xrow = (((int64_t)pn * g.H + hi0) * g.W + wi0) * g.C + c0 + sch * 8;
+    __bf16* st = smem + slot * WG_STAGE;
+    glds16(in ? (const void*)(DY + pm * g.K + k0 + sch * 8) : (const void*)zaddr,
+           st + (wid * 64) * 8);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int r = tap / 3, s = tap % 3;
+      const bool ok = in && (unsigned)(hi0 + r) < (unsigned)g.H && (unsigned)(wi0 + s) < (unsigned)g.W;
+      const uint64_t a = ok ? (uint64_t)(X + xrow + ((int64_t)r * g.W + s) * g.C) : zaddr;
+      glds16((const void*)a, st + ((1 + tap) * WG_NT + wid * 64) * 8);
+    }
+    // advance this thread's row by one stage (32 pixels)
+    pm += WG_ROWS;
+    pwo += WG_ROWS;
+    while (pwo >= g.Wo) {
+      pwo -= g.Wo;
+      if (++pho == g.Ho) {
+        pho = 0;
+        ++pn;
+      }
+    }
+  };
+
+  const int ct = wid;
+  const int gq = lane >> 4, cl = lane & 15;
+  f32x4v acc[9][4];
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[tp][u] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  if (ch0 < ch1) {
+    // 2-slot ring: stage j+1 is issued right after the barrier that retires stage j
+    // (and frees slot (j+1) % 2) and lands while stage j is multiplied
+    issue(0);
+    int slot = 0;
+    for (int64_t chk = ch0; chk < ch1; ++chk) {
+      wait_vm<0>();
+      raw_barrier();
+      if (chk + 1 < ch1) issue(slot ^ 1);
+      const __bf16* st = smem + slot * WG_STAGE;
+      bf16x8 af[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) af[u] = tr8(st, 8 * gq, 8 * gq + 4, 16 * u, cl);
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        const bf16x8 bfr = tr8(st + (1 + tp) * WG_TILE, 8 * gq, 8 * gq + 4, 16 * ct, cl);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[tp][u] = mfma(af[u], bfr, acc[tp][u]);
+      }
+      slot ^= 1;
+    }
+    wait_vm<0>();
+  }
+  // partial[ms][tap][k][c] (fp32, this block's 64 x 64 window); every block writes its
+  // window even with no chunks (zeros) so the reduce never reads garbage
+  float* pb = partial + (int64_t)ms * 9 * g.K * g.C;
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + 16 * u + 4 * gq + r, c = c0 + 16 * ct + cl;
+        pb[((int64_t)tp * g.K + k) * g.C + c] = acc[tp][u][r];
+      }
+}
+
+// dw[k][tap][c] (bf16) = sum over the m splits, fixed order
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial,
+                                                            __bf16* __restrict__ dw, int K, int C,
+                                                            int msplit) {
+  const int64_t n = (int64_t)9 * K * C;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;    // index in [tap][k][c]
+  if (i >= n) return;
+  float s = 0.f;
+  for (int p = 0; p < msplit; ++p) s += partial[(int64_t)p * n + i];
+  const int c = (int)(i % C);
+  const int64_t tk = i / C;
+  const int k = (int)(tk % K), tap = (int)(tk / K);
+  dw[((int64_t)k * 9 + tap) * C + c] = (__bf16)s;
+}
+
+}  // namespace conv
+}  // namespace mv
+
+static int wgrad_msplit(int64_t nchunks, int nkc) {
+  const char* e = std::getenv("MIVOD_WGRAD_BLOCKS");       // workgroups per launch (A/B)
+  const int64_t target = e && std::atoi(e) > 0 ? std::atoi(e) : 512;
+  int64_t ms = target / nkc;
+  if (ms < 1) ms = 1;
+  if (ms > nchunks) ms = nchunks;
+  return (int)ms;
+}
+
+int64_t mv_wgrad3x3_workspace(int64_t M, int K, int C) {
+  const int nkc = (K / 64) * (C / 64);
+  const int64_t nchunks = (M + 31) / 32;
+  return (int64_t)wgrad_msplit(nchunks, nkc) * 9 * K * C;
+}
+
+bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
+                 int K, int stride, hipStream_t st) {
+  using namespace mv::conv;
+  if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2)) return false;
+  Geo g;
+  g.H = H;
+  g.W = W;
+  g.C = C;
+  g.K = K;
+  g.st = stride;
+  g.Ho = (H - 1) / stride + 1;
+  g.Wo = (W - 1) / stride + 1;
+  g.M = (int64_t)N * g.Ho * g.Wo;
+  const int nkc = (K / 64) * (C / 64);
+  const int64_t nchunks = (g.M + 31) / 32;
+  const int ms = wgrad_msplit(nchunks, nkc);
+  hipLaunchKernelGGL(wgrad3x3_kernel, dim3((unsigned)(nkc * ms)), dim3(WG_NT), 0, st,
+                     (const __bf16*)x, (const __bf16*)dy, work, g, nkc, ms, nchunks);
+  const int64_t n = (int64_t)9 * K * C;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     (const float*)work, (__bf16*)dw, K, C, ms);
+  return true;
+}

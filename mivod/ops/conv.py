@@ -197,6 +197,14 @@ def _dgrad_on_mivod(cin: int, cout: int) -> bool:
     return os.environ.get("MIVOD_CONV3X3_DGRAD", "1") != "0" and max(cin, cout) <= 128
 
 
+def _wgrad_on_mivod(cin: int, cout: int, stride: int) -> bool:
+    """mivod's 3x3 weight-gradient kernel (csrc/kernels/mv_conv.hip wgrad3x3_kernel) beats
+    MIOpen's on every ResNet-50 conv2 shape except the 512-channel stride-2 one
+    (scripts/micro_conv3x3.py: 608-793 vs 393-743 TF/s)."""
+    return (os.environ.get("MIVOD_WGRAD3X3", "1") != "0"
+            and not (stride == 2 and max(cin, cout) >= 512))
+
+
 class _Conv3x3(torch.autograd.Function):
     """y = conv3x3(x, w, stride, pad 1) on mivod's implicit-GEMM kernel (csrc/kernels/
     mv_conv.hip), optionally with the following BatchNorm's statistics partials of y
@@ -205,8 +213,8 @@ class _Conv3x3(torch.autograd.Function):
     kernel for <= 128 channels, MIOpen's forward solver otherwise) — and when x is the
     output of a fused BN+ReLU (``slot``, mode 1), mivod's kernel also runs that BN's
     backward reduce in its epilogue and hands (d, partials) to it through the slot, the
-    same protocol as ``_Conv1x1BN``; stride-2 data gradient and the weight gradient
-    from MIOpen."""
+    same protocol as ``_Conv1x1BN``; the weight gradient on mivod's wgrad3x3 kernel
+    (MIOpen for the 512-channel stride-2 conv); stride-2 data gradient from MIOpen."""
 
     @staticmethod
     def forward(ctx, x, w, stride, shift, stats, slot):
@@ -251,12 +259,17 @@ class _Conv3x3(torch.autograd.Function):
                         dx = K.native().conv3x3(dy, wt, 1)
                 else:
                     dx = F.conv2d(dy, wt, None, 1, 1)
-            if need_w:
-                _, dw, _ = torch.ops.aten.convolution_backward(
-                    dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
         else:
-            dx, dw, _ = torch.ops.aten.convolution_backward(
-                dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [need_x, need_w, False])
+            if need_x:
+                dx, _, _ = torch.ops.aten.convolution_backward(
+                    dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])
+        if need_w:
+            if _wgrad_on_mivod(w.shape[1], w.shape[0], s):
+                from . import kernels as K
+                dw = K.native().wgrad3x3(x, dy, s)
+            else:
+                _, dw, _ = torch.ops.aten.convolution_backward(
+                    dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
         return dx, dw, None, None, None, None
 
 

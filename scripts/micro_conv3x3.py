@@ -7,7 +7,7 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+import bench  # noqa: E402,F401  (stages the shipped MIOpen find-db / kernel cache like the bench)
 torch.backends.cudnn.benchmark = True
 from mivod.ops import kernels as K  # noqa: E402
 
@@ -59,3 +59,30 @@ for h, c, k, s, cnt in SH:
     del x, y, ref
     torch.cuda.empty_cache()
 print(f"per step: conv2d {tot[0] / 1e3:.2f} ms, mivod {tot[1] / 1e3:.2f} ms, +stats {tot[2] / 1e3:.2f} ms")
+
+# ---- weight gradient: MIOpen (aten.convolution_backward, weight only) vs mivod wgrad3x3
+tw = [0.0, 0.0]
+for h, c, k, s, cnt in SH:
+    x = (torch.randn(BS, c, h, h, device=dev) * 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(k, c, 3, 3, device=dev) / (9 * c) ** 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    ho = (h - 1) // s + 1
+    dy = torch.randn(BS, k, ho, ho, device=dev).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    t_ref = bench(lambda: torch.ops.aten.convolution_backward(
+        dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
+    t_mv = bench(lambda: nat.wgrad3x3(x, dy, s))
+    ref = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False,
+                                              [0, 0], 1, [False, True, False])[1]
+    got = nat.wgrad3x3(x, dy, s)
+    err = ((got.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
+    fl = 2 * BS * ho * ho * k * 9 * c
+    n_w = cnt // 2 if s == 1 else cnt     # SH counts fwd + dgrad launches for stride 1
+    tw[0] += t_ref * n_w
+    tw[1] += t_mv * n_w
+    print(f"wgrad H{h:3d} {c:4d}->{k:4d} s{s}: miopen {t_ref:8.1f} us ({fl / t_ref / 1e6:6.1f} TF/s) | "
+          f"mivod {t_mv:8.1f} us ({fl / t_mv / 1e6:6.1f} TF/s) | rel err {err:.1e}", flush=True)
+    del x, dy
+    torch.cuda.empty_cache()
+print(f"wgrad per step: miopen {tw[0] / 1e3:.2f} ms, mivod {tw[1] / 1e3:.2f} ms")

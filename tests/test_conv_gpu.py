@@ -145,3 +145,19 @@ def test_resnet_uses_conv3x3_bwd_fusion(cuda, monkeypatch):
     x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
     F.cross_entropy(m(x).float(), torch.randint(0, 10, (4,), device=cuda)).backward()
     assert len(calls) == 3, calls       # layer1.0, layer1.1, layer2.1 (layer2.0 is strided)
+
+
+@pytest.mark.parametrize("n,c,k,h,w,s", [(2, 64, 64, 9, 7, 1), (3, 128, 128, 10, 10, 2),
+                                         (2, 64, 128, 8, 8, 1), (1, 256, 64, 7, 7, 1)])
+def test_wgrad3x3_matches_fp32(cuda, n, c, k, h, w, s):
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(n + c + k + h + s)
+    x = _cl(torch.randn(n, c, h, w, device=cuda, generator=g).to(torch.bfloat16))
+    ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+    dy = _cl(torch.randn(n, k, ho, wo, device=cuda, generator=g).to(torch.bfloat16))
+    wref = torch.zeros(k, c, 3, 3, device=cuda, requires_grad=True)
+    F.conv2d(x.float(), wref, None, s, 1).backward(dy.float())
+    dw = nat.wgrad3x3(x, dy, s)
+    assert dw.shape == (k, c, 3, 3) and dw.is_contiguous(memory_format=torch.channels_last)
+    ref = wref.grad
+    torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
