@@ -25,11 +25,15 @@ struct PoolGeo {
   int N, H, W, C, OH, OW, k, s, p;
 };
 
+// KC > 0: compile-time window size (ResNet's 3): the KC*KC loads are unrolled and all in
+// flight at once instead of one dependent load per loop trip
+template <int KC>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restrict__ x,
                                                           const float* __restrict__ scale,
                                                           const float* __restrict__ bias,
                                                           int relu, __bf16* __restrict__ y,
                                                           uint8_t* __restrict__ idx, PoolGeo g) {
+  const int k = KC > 0 ? KC : g.k;
   const int cv = g.C / 8;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)g.N * g.OH * g.OW * cv;
@@ -55,15 +59,17 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restri
 #pragma unroll
   for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
   const int h0 = oh * g.s - g.p, w0 = ow * g.s - g.p;
-  for (int kh = 0; kh < g.k; ++kh) {
+#pragma unroll
+  for (int kh = 0; kh < k; ++kh) {
     const int ih = h0 + kh;
     if (ih < 0 || ih >= g.H) continue;
-    for (int kw = 0; kw < g.k; ++kw) {
+#pragma unroll
+    for (int kw = 0; kw < k; ++kw) {
       const int iw = w0 + kw;
       if (iw < 0 || iw >= g.W) continue;
       float v[8];
       load8(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c, v);
-      const uint32_t pos = kh * g.k + kw;
+      const uint32_t pos = kh * k + kw;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float a = scale ? __builtin_fmaf(v[j], sc[j], bi[j]) : v[j];
@@ -136,6 +142,79 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restri
     }
   }
   store8(dx + t * 8, acc);
+}
+
+// k = 3, s = 2, p = 1 (ResNet) with even H, W: one lane per 2x2 block of input pixels
+// x 8 channels.  The block (2a.., 2b..) belongs to exactly the windows oh in {a, a+1},
+// ow in {b, b+1}, so every lane loads the same 4 windows (no divergent 1/2/4-window
+// loops as in the generic kernel, and each window's dy / index is loaded once per block
+// instead of once per covered pixel) and writes 4 pixels.
+__global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(const __bf16* __restrict__ dy,
+                                                               const __bf16* __restrict__ dy2,
+                                                               const uint8_t* __restrict__ idx,
+                                                               __bf16* __restrict__ dx,
+                                                               PoolGeo g) {
+  const uint32_t cv = (uint32_t)g.C / 8, hb = (uint32_t)g.H / 2, wb = (uint32_t)g.W / 2;
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t total = (uint32_t)g.N * hb * wb * cv;
+  if (t >= total) return;
+  const uint32_t q0 = t / cv;
+  const int c = (int)(t - q0 * cv) * 8;
+  const uint32_t q1 = q0 / wb;
+  const int b = (int)(q0 - q1 * wb);
+  const uint32_t n = q1 / hb;
+  const int a = (int)(q1 - n * hb);
+  float acc[2][2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[i][jj][e] = 0.f;
+#pragma unroll
+  for (int da = 0; da < 2; ++da) {
+    const int oh = a + da;
+    if (oh >= g.OH) continue;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int ow = b + db;
+      if (ow >= g.OW) continue;
+      const int64_t o = (((int64_t)n * g.OH + oh) * g.OW + ow) * g.C + c;
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 iw8 = *reinterpret_cast<const u32x2*>(idx + o);
+      float d[8];
+      load8(dy + o, d);
+      if (dy2) {
+        float e2[8];
+        load8(dy2 + o, e2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] += e2[e];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int kh = i - 2 * da + 1;          // row of input 2a + i inside window oh
+        if (kh < 0) continue;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int kw = jj - 2 * db + 1;
+          if (kw < 0) continue;
+          const uint32_t pos = (uint32_t)(kh * 3 + kw);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t w = e < 4 ? iw8[0] : iw8[1];
+            if (((w >> (8 * (e & 3))) & 0xffu) == pos) acc[i][jj][e] += d[e];
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int64_t px = ((int64_t)n * g.H + 2 * a + i) * g.W + 2 * b + jj;
+      store8(dx + px * g.C + c, acc[i][jj]);
+    }
 }
 
 // global average pool: x [N, HW, C] -> y [N, C]; one lane per (n, 8 channels)
@@ -218,8 +297,12 @@ void mv_maxpool_fwd(const void* x, const float* scale, const float* bias, bool r
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
   if (total >= (int64_t(1) << 32)) return;   // bindings reject such shapes first
   if (!total) return;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
-                     (const __bf16*)x, scale, bias, relu ? 1 : 0, (__bf16*)y, idx, g);
+  if (k == 3)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<3>, dim3(blocks_for(total)), dim3(256), 0, st,
+                       (const __bf16*)x, scale, bias, relu ? 1 : 0, (__bf16*)y, idx, g);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<0>, dim3(blocks_for(total)), dim3(256), 0, st,
+                       (const __bf16*)x, scale, bias, relu ? 1 : 0, (__bf16*)y, idx, g);
 }
 
 void mv_maxpool_bwd(const void* dy, const void* dy2, const uint8_t* idx, void* dx, int N, int H,
@@ -228,6 +311,12 @@ void mv_maxpool_bwd(const void* dy, const void* dy2, const uint8_t* idx, void* d
   const int64_t total = (int64_t)N * H * W * (C / 8);
   if (!total) return;
   if (total >= (int64_t(1) << 32)) return;   // bindings reject such shapes first
+  if (k == 3 && s == 2 && p == 1 && H % 2 == 0 && W % 2 == 0 && OH == H / 2 && OW == W / 2) {
+    const int64_t t4 = total / 4;
+    hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel, dim3(blocks_for(t4)), dim3(256), 0, st,
+                       (const __bf16*)dy, (const __bf16*)dy2, idx, (__bf16*)dx, g);
+    return;
+  }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
                      (const __bf16*)dy, (const __bf16*)dy2, idx, (__bf16*)dx, g);
 }
