@@ -113,7 +113,7 @@ __device__ __forceinline__ void raw_barrier() {
 // of the BN whose output was this conv's input: y is the data gradient dy of that output,
 // d = (x_bn * scale + bias > 0) ? bf16(dy) : 0 is written instead, partials (sum d,
 // sum d (x_bn - mean)) — mv_bn.hip's bwd_reduce_kernel<1> folded into the epilogue.
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI, int NS = 3>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Wt, __bf16* __restrict__ Y, Geo g,
     int ntn, int64_t ntm, const float* __restrict__ shift, float* __restrict__ partial,
@@ -126,7 +126,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
   constexpr int B_CH = BN * 8 / NT;
   constexpr int LPS = A_CH + B_CH;                // glds per thread per stage
   constexpr int STAGE = (BM + BN) * BK;
-  constexpr int NS = 3;                           // LDS ring: 2 stages in flight
+  static_assert(NS == 2 || NS == 3, "LDS ring: 2 slots (1 stage in flight, 2 workgroups per "
+                                     "CU) or 3 slots (2 stages in flight)");
   __shared__ __attribute__((aligned(16))) __bf16 smem[NS * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
       ikt = k2;
       return true;
     };
-    bool ahead = issue_next();      // stage of step 1 in flight
+    bool ahead = NS == 3 ? issue_next() : false;   // 3 slots: stage of step 1 in flight
     int slot = 0;
     while (true) {
 #pragma unroll
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
 #pragma unroll
         for (int b = 0; b < TM; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
       for (int kt = 0; kt < KT; ++kt) {
-        if (ahead) wait_vm<LPS>(); else wait_vm<0>();
+        if (NS == 3 && ahead) wait_vm<LPS>(); else wait_vm<0>();
         raw_barrier();          // this step's stage is visible to all; the oldest slot is free
         ahead = issue_next();
         const __bf16* As = smem + slot * STAGE;
@@ -326,17 +327,17 @@ template <int BN, bool STATS>
 struct Cfg;
 template <bool STATS>
 struct Cfg<128, STATS> {
-  static constexpr int BM = 256, WM = 4, WN = 2;
+  static constexpr int BM = 128, WM = 2, WN = 2, NS = 2;    // 64 KB: 2 workgroups per CU
 };
 template <bool STATS>
 struct Cfg<64, STATS> {
-  static constexpr int BM = 256, WM = 4, WN = 2;
+  static constexpr int BM = 256, WM = 4, WN = 2, NS = 2;    // 80 KB: 2 workgroups per CU
 };
 
 template <int BN, bool STATS, int EPI = STATS ? 1 : 0>
 static const void* kernel_ptr() {
   using C = Cfg<BN, STATS>;
-  return (const void*)&conv3x3_kernel<C::BM, BN, C::WM, C::WN, EPI>;
+  return (const void*)&conv3x3_kernel<C::BM, BN, C::WM, C::WN, EPI, C::NS>;
 }
 
 template <int BN, bool STATS>
@@ -397,15 +398,16 @@ bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int 
 #define MV_LAUNCH(BNV, ST)                                                                     \
   {                                                                                            \
     constexpr int BMV = Cfg<BNV, ST>::BM, WMV = Cfg<BNV, ST>::WM, WNV = Cfg<BNV, ST>::WN;      \
+    constexpr int NSV = Cfg<BNV, ST>::NS;                                                      \
     const int64_t ntm = (g.M + BMV - 1) / BMV;                                                 \
     const int ntn = K / BNV;                                                                   \
     const int64_t ns = streams_for<BNV, ST>(ntm, ntn);                                         \
     if (BX)                                                                                    \
-      hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, WNV, 2>), dim3((unsigned)(ns * ntn)),     \
+      hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, WNV, 2, NSV>), dim3((unsigned)(ns * ntn)),\
                          dim3(WMV * WNV * 64), 0, st, X, Wt, Y, g, ntn, ntm, shift, partial, BX, \
                          bn_vec);                                                              \
     else                                                                                       \
-      hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, WNV, ST ? 1 : 0>),                       \
+      hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, WNV, ST ? 1 : 0, NSV>),                  \
                          dim3((unsigned)(ns * ntn)), dim3(WMV * WNV * 64), 0, st, X, Wt, Y, g,   \
                          ntn, ntm, shift, partial, BX, bn_vec);                                \
   }

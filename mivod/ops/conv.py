@@ -178,6 +178,12 @@ def conv1x1_stats(m: nn.Conv2d, x: torch.Tensor, shift):
 
 
 # ---------------------------------------------------------------- 3x3 implicit GEMM
+# bench.py A/B (1 box, 2 runs each): data gradient on MIOpen 13,219-13,238 img/s, on mivod
+# for <= 64 / <= 128 channels 13,129-13,132 / 13,040-13,091, always 12,809-12,869: the
+# BN-reduce epilogue variant is not yet ahead in the full step, so MIOpen keeps it
+_DGRAD_DEFAULT = "0"
+
+
 def conv3x3_eligible(m: nn.Conv2d, x: torch.Tensor) -> bool:
     """3x3 / pad 1 / stride 1-2 convs on channels_last bf16 GPU tensors with channel
     counts that are multiples of 64 (every ResNet-50 bottleneck conv2)."""
@@ -191,10 +197,16 @@ def conv3x3_eligible(m: nn.Conv2d, x: torch.Tensor) -> bool:
 
 
 def _dgrad_on_mivod(cin: int, cout: int) -> bool:
-    """The stride-1 data gradient (a forward 3x3 conv Cout -> Cin) runs on mivod's kernel
-    where it beats MIOpen's forward solver (scripts/micro_conv3x3.py: 64- and 128-channel
-    layers); wider layers keep MIOpen."""
-    return os.environ.get("MIVOD_CONV3X3_DGRAD", "1") != "0" and max(cin, cout) <= 128
+    """Whether the stride-1 data gradient (a forward 3x3 conv Cout -> Cin) runs on mivod's
+    kernel — which also lets it carry the producing BN's backward reduce — instead of
+    MIOpen's forward solver.  MIVOD_CONV3X3_DGRAD: 0 = never, 1 = always, N = up to N
+    channels (default: see _DGRAD_DEFAULT, chosen by bench.py A/B)."""
+    v = os.environ.get("MIVOD_CONV3X3_DGRAD", _DGRAD_DEFAULT)
+    if v == "0":
+        return False
+    if v == "1":
+        return True
+    return max(cin, cout) <= int(v)
 
 
 def _wgrad_on_mivod(cin: int, cout: int, stride: int) -> bool:

@@ -129,7 +129,7 @@ def test_conv3x3_bn_bwd_matches_reference(cuda, c, k):
 
 
 def test_resnet_uses_conv3x3_bwd_fusion(cuda, monkeypatch):
-    """conv2's data gradient carries BN1's backward reduce on the <=128-channel layers."""
+    """conv2's data gradient carries BN1's backward reduce on every stride-1 conv2."""
     from mivod.models.resnet import ResNet, to_mixed_bf16
     nat = _nat()
     calls = []
@@ -140,11 +140,12 @@ def test_resnet_uses_conv3x3_bwd_fusion(cuda, monkeypatch):
         return real(*a)
 
     monkeypatch.setattr(nat, "conv3x3_bn_bwd", counted)
+    monkeypatch.setenv("MIVOD_CONV3X3_DGRAD", "1")     # off by default (bench A/B)
     torch.manual_seed(0)
     m = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
     x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
     F.cross_entropy(m(x).float(), torch.randint(0, 10, (4,), device=cuda)).backward()
-    assert len(calls) == 3, calls       # layer1.0, layer1.1, layer2.1 (layer2.0 is strided)
+    assert len(calls) == 4, calls       # layer1.0, layer1.1, layer2.1, layer3.1 (x.0: stride 2)
 
 
 @pytest.mark.parametrize("n,c,k,h,w,s", [(2, 64, 64, 9, 7, 1), (3, 128, 128, 10, 10, 2),

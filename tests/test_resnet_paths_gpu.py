@@ -14,7 +14,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 _KEYS = ("MIVOD_FUSED_BN", "MIVOD_CONV_DGRAD_FWD", "MIVOD_BN_TAP", "MIVOD_DOWNSAMPLE_TAP",
-         "MIVOD_CONV_BN_FUSE", "MIVOD_CONV_BN_BWD_FUSE", "MIVOD_CONV3X3")
+         "MIVOD_CONV_BN_FUSE", "MIVOD_CONV_BN_BWD_FUSE", "MIVOD_CONV3X3", "MIVOD_WGRAD3X3")
 
 
 def _grads(model, x, y, monkeypatch, fused, fp32=False):
