@@ -925,16 +925,30 @@ std::vector<at::Tensor> bn_bwd_from_partials(at::Tensor dz, at::Tensor x, at::Te
 // ---------------------------------------------------------------------------
 int64_t conv3x3_partials(int64_t M, int64_t K) { return mv_conv3x3_partials(M, (int)K); }
 
-// y = conv3x3(x, w, stride, pad 1) (+ BN statistics partials of y around shift)
+// y = conv3x3(x, w, stride, pad 1) / conv1x1(x, w, stride) (+ BN statistics partials of y
+// around shift)
+at::Tensor conv_nhwc(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> shift,
+                     c10::optional<at::Tensor> partial, int64_t ks);
+
 at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> shift,
                    c10::optional<at::Tensor> partial) {
+  return conv_nhwc(x, w, stride, shift, partial, 3);
+}
+
+at::Tensor conv1x1_mfma(at::Tensor x, at::Tensor w, int64_t stride,
+                        c10::optional<at::Tensor> shift, c10::optional<at::Tensor> partial) {
+  return conv_nhwc(x, w, stride, shift, partial, 1);
+}
+
+at::Tensor conv_nhwc(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> shift,
+                     c10::optional<at::Tensor> partial, int64_t ks) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv3x3: x must be a channels_last bf16 GPU tensor [N, C, H, W]");
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 &&
-                  w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+                  w.size(2) == ks && w.size(3) == ks && w.size(1) == x.size(1) &&
                   w.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "conv3x3: w must be a channels_last bf16 [K, C, 3, 3] filter matching x");
+              "conv: w must be a channels_last bf16 [K, C, ks, ks] filter matching x");
   TORCH_CHECK(w.device() == x.device(), "conv3x3: devices differ");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = w.size(0);
   TORCH_CHECK(C % 64 == 0 && K % 64 == 0 && C > 0 && K > 0, "conv3x3: C and K must be multiples of 64");
@@ -961,9 +975,9 @@ at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at:
       sp = shift->data_ptr<float>();
     }
   }
-  TORCH_CHECK(mv_conv3x3(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)C,
-                         (int)K, (int)stride, sp, pp, cur_stream()),
-              "conv3x3: unsupported shape");
+  TORCH_CHECK(mv_conv_nhwc(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W,
+                           (int)C, (int)K, (int)ks, (int)stride, sp, pp, cur_stream()),
+              "conv: unsupported shape");
   return y;
 }
 
@@ -1079,6 +1093,9 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("bn_bwd_from_partials", &bn_bwd_from_partials,
         "BN backward finalize + dx from GEMM-epilogue partials -> (dx, dgamma, dbeta)");
   m.def("conv3x3", &conv3x3, "implicit-GEMM 3x3 conv (pad 1) with optional fused BN statistics",
+        py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("shift") = py::none(),
+        py::arg("partial") = py::none());
+  m.def("conv1x1", &conv1x1_mfma, "1x1 conv (implicit-GEMM kernel) with optional fused BN statistics",
         py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("shift") = py::none(),
         py::arg("partial") = py::none());
   m.def("conv3x3_bn_bwd", &conv3x3_bn_bwd,

@@ -16,6 +16,11 @@ bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int 
                 int stride, const float* shift, float* partial, hipStream_t st,
                 const void* bn_x = nullptr, const float* bn_vec = nullptr);
 
+// same kernel for ks = 1 (pad 0) or 3 (pad 1): y[N, Ho, Wo, K] = conv(x[N, H, W, C], w[K, ks, ks, C])
+bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, int C, int K, int ks,
+                  int stride, const float* shift, float* partial, hipStream_t st,
+                  const void* bn_x = nullptr, const float* bn_vec = nullptr);
+
 // 3x3 weight gradient: dw[K, 3, 3, C] (bf16, channels_last [K, C, 3, 3]) of
 // y = conv3x3(x, w, stride, pad 1) given dy; work: fp32 [mv_wgrad3x3_workspace(M, K, C)]
 int64_t mv_wgrad3x3_workspace(int64_t M, int K, int C);

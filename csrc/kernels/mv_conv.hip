@@ -59,6 +59,7 @@ __device__ __forceinline__ void glds16(const void* src, __bf16* lds_wave_base) {
 struct Geo {
   int H, W, C, Ho, Wo, K, st;
   int64_t M;
+  int ks = 3;        // filter size: 3 (pad 1) or 1 (pad 0) for the forward kernel
 };
 
 // per-thread state of the A rows it stages (A_CH rows, fixed source chunk): the byte
@@ -83,14 +84,16 @@ __device__ __forceinline__ void row_info(const Geo& g, const __bf16* X, int64_t 
       const int n = (int)(m / hw);
       const int rem = (int)(m - (int64_t)n * hw);
       const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
-      const int hi0 = ho * g.st - 1, wi0 = wo * g.st - 1;
+      const int pad = g.ks >> 1;
+      const int hi0 = ho * g.st - pad, wi0 = wo * g.st - pad;
       uint32_t v = 0;
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
-          const bool ok = (unsigned)(hi0 + r) < (unsigned)g.H && (unsigned)(wi0 + s) < (unsigned)g.W;
-          v |= (ok ? 1u : 0u) << (r * 3 + s);
+          const bool ok = r < g.ks && s < g.ks && (unsigned)(hi0 + r) < (unsigned)g.H &&
+                          (unsigned)(wi0 + s) < (unsigned)g.W;
+          v |= (ok ? 1u : 0u) << (r * g.ks + s);
         }
       ri.valid[i] = v;
       ri.addr[i] = (uint64_t)(X + ((((int64_t)n * g.H + hi0) * g.W + wi0) * g.C + sc * 8));
@@ -137,8 +140,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
   const int nt = t % ntn;
   const int64_t stream = t / ntn, nstreams = gridDim.x / ntn;
   const int n0 = nt * BN;
-  const int csteps = g.C / BK, KT = 9 * csteps;
-  const int64_t wrow = (int64_t)9 * g.C;          // filter row length
+  const int taps = g.ks * g.ks;
+  const int csteps = g.C / BK, KT = taps * csteps;
+  const int64_t wrow = (int64_t)taps * g.C;       // filter row length
   const int sc = (tid & 7) ^ ((tid >> 3) & 7);    // swizzled source chunk of this thread
 
   uint64_t brow[B_CH];                            // filter rows of this thread
@@ -149,7 +153,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
 
   auto issue = [&](const RowInfo<A_CH>& ri, int kt, int buf) {
     const int tap = kt / csteps, c0 = (kt - tap * csteps) * BK;   // wave-uniform
-    const int r = tap / 3, s = tap - r * 3;
+    const int r = tap / g.ks, s = tap - r * g.ks;
     const int64_t offa = (((int64_t)r * g.W + s) * g.C + c0) * 2;
     const int64_t offb = ((int64_t)tap * g.C + c0) * 2;
     __bf16* As = smem + buf * STAGE;
@@ -379,15 +383,23 @@ int64_t mv_conv3x3_partials(int64_t M, int K) {
 bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int C, int K,
                 int stride, const float* shift, float* partial, hipStream_t st,
                 const void* bn_x, const float* bn_vec) {
+  return mv_conv_nhwc(x, w, y, N, H, W, C, K, 3, stride, shift, partial, st, bn_x, bn_vec);
+}
+
+bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, int C, int K, int ks,
+                  int stride, const float* shift, float* partial, hipStream_t st,
+                  const void* bn_x, const float* bn_vec) {
   using namespace mv::conv;
-  if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2)) return false;
+  if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2) || (ks != 1 && ks != 3))
+    return false;
   Geo g;
+  g.ks = ks;
   g.H = H;
   g.W = W;
   g.C = C;
   g.K = K;
   g.st = stride;
-  g.Ho = (H - 1) / stride + 1;
+  g.Ho = (H - 1) / stride + 1;   // (H + 2 (ks / 2) - ks) / stride + 1 for ks = 1, 3
   g.Wo = (W - 1) / stride + 1;
   g.M = (int64_t)N * g.Ho * g.Wo;
   const __bf16* X = (const __bf16*)x;

@@ -10,7 +10,7 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+import bench  # noqa: E402,F401  (stages the shipped MIOpen find-db / kernel cache like the bench)
 torch.backends.cudnn.benchmark = True
 from mivod.ops import kernels as K  # noqa: E402
 
@@ -130,3 +130,23 @@ for hw, k, n, cnt in BW:
     torch.cuda.empty_cache()
 print(f"bwd per step: unfused {tb[0] / 1e3:.2f} ms, fused {tb[1] / 1e3:.2f} ms -> saving "
       f"{(tb[0] - tb[1]) / 1e3:.2f} ms")
+
+# ---- forward on the implicit-GEMM conv kernel (ks = 1) for the large-K 1x1 shapes
+print("-- conv kernel (ks=1) forward")
+for hw, cin, cout, cnt in SH:
+    if cin < 512:
+        continue
+    x = (torch.randn(BS, cin, hw, hw, device=dev) * 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, 1, 1, device=dev) / cin ** 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    M = BS * hw * hw
+    part = torch.empty(nat.conv3x3_partials(M, cout), 2, cout, device=dev)
+    t_conv = bench(lambda: F.conv2d(x, w))
+    t_mv = bench(lambda: nat.conv1x1(x, w, 1))
+    t_st = bench(lambda: nat.conv1x1(x, w, 1, None, part))
+    fl = 2 * M * cin * cout
+    print(f"1x1 M={M:8d} K={cin:4d} N={cout:4d} x{cnt}: conv2d {t_conv:7.1f} us ({fl / t_conv / 1e6:6.1f} TF/s) | "
+          f"mivod {t_mv:7.1f} us ({fl / t_mv / 1e6:6.1f} TF/s) | +stats {t_st:7.1f} us", flush=True)
+    del x
+    torch.cuda.empty_cache()

@@ -162,3 +162,23 @@ def test_wgrad3x3_matches_fp32(cuda, n, c, k, h, w, s):
     assert dw.shape == (k, c, 3, 3) and dw.is_contiguous(memory_format=torch.channels_last)
     ref = wref.grad
     torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("n,c,k,h,w,s", [(2, 512, 128, 9, 7, 1), (3, 1024, 256, 7, 7, 1),
+                                         (2, 256, 512, 10, 10, 2), (1, 64, 64, 5, 6, 1)])
+def test_conv1x1_kernel_matches_fp32(cuda, n, c, k, h, w, s):
+    """The implicit-GEMM kernel with ks = 1 (pad 0) against an fp32 1x1 conv, + statistics."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(n + c + k + s)
+    x = _cl(torch.randn(n, c, h, w, device=cuda, generator=g).to(torch.bfloat16))
+    wt = _cl((torch.randn(k, c, 1, 1, device=cuda, generator=g) / c ** 0.5).to(torch.bfloat16))
+    ref = F.conv2d(x.float(), wt.float(), None, s)
+    y = nat.conv1x1(x, wt, s)
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    M = ref.shape[0] * ref.shape[2] * ref.shape[3]
+    part = torch.full((nat.conv3x3_partials(M, k), 2, k), float("nan"), device=cuda)
+    y2 = nat.conv1x1(x, wt, s, None, part)
+    assert torch.equal(y, y2)
+    d = y.float().permute(0, 2, 3, 1).reshape(-1, k)
+    torch.testing.assert_close(part.sum(0)[0], d.sum(0), rtol=1e-4, atol=1e-2)
