@@ -116,8 +116,11 @@ __device__ __forceinline__ void raw_barrier() {
 // of the BN whose output was this conv's input: y is the data gradient dy of that output,
 // d = (x_bn * scale + bias > 0) ? bf16(dy) : 0 is written instead, partials (sum d,
 // sum d (x_bn - mean)) — mv_bn.hip's bwd_reduce_kernel<1> folded into the epilogue.
+// the second launch bound asks for 2 resident workgroups (the LDS ring allows 2): the
+// 8-wave BN-reduce variant otherwise grows past 128 VGPRs and runs one workgroup per CU
 template <int BM, int BN, int WM, int WN, int EPI, int NS = 3>
-__global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
+__global__ __launch_bounds__(WM * WN * 64)
+__attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void conv3x3_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Wt, __bf16* __restrict__ Y, Geo g,
     int ntn, int64_t ntm, const float* __restrict__ shift, float* __restrict__ partial,
     const __bf16* __restrict__ bnx, const float* __restrict__ bnvec) {
@@ -168,19 +171,15 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
   };
 
   const int gq = lane >> 4, rl = lane & 15;
-  float sh[TN][4], s1[TN][4], s2[TN][4];
-  float bsc[EPI == 2 ? TN : 1][4], bbi[EPI == 2 ? TN : 1][4];
+  // EPI 2 reads its per-channel (mean, scale, bias) in the epilogue from the cache: held
+  // in registers across the K loop they pushed the kernel past 2 waves per SIMD
+  float sh[EPI == 1 ? TN : 1][4], s1[TN][4], s2[TN][4];
 #pragma unroll
   for (int a = 0; a < TN; ++a)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int col = n0 + wn * WTN + a * 16 + 4 * gq + r;
-      sh[a][r] = (EPI == 1 && shift) ? shift[col] : 0.f;
-      if constexpr (EPI == 2) {
-        sh[a][r] = bnvec[col];                   // saved mean
-        bsc[a][r] = bnvec[2 * g.K + col];        // scale = gamma * invstd
-        bbi[a][r] = bnvec[3 * g.K + col];        // bias = beta - mean * scale
-      }
+      if constexpr (EPI == 1) sh[a][r] = shift ? shift[col] : 0.f;
       s1[a][r] = 0.f;
       s2[a][r] = 0.f;
     }
@@ -260,14 +259,20 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_kernel(
               const u32x2 xw = *reinterpret_cast<const u32x2*>(bnx + row * g.K + col);
               const float xv[4] = {__uint_as_float(xw[0] << 16), __uint_as_float(xw[0] & 0xffff0000u),
                                    __uint_as_float(xw[1] << 16), __uint_as_float(xw[1] & 0xffff0000u)};
+              const float4 mu = *reinterpret_cast<const float4*>(bnvec + col);
+              const float4 sc4 = *reinterpret_cast<const float4*>(bnvec + 2 * g.K + col);
+              const float4 bi4 = *reinterpret_cast<const float4*>(bnvec + 3 * g.K + col);
+              const float mus[4] = {mu.x, mu.y, mu.z, mu.w};
+              const float scs[4] = {sc4.x, sc4.y, sc4.z, sc4.w};
+              const float bis[4] = {bi4.x, bi4.y, bi4.z, bi4.w};
               float dv[4];
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float d =
-                    __builtin_fmaf(xv[r], bsc[a][r], bbi[a][r]) > 0.f ? round_bf16(v[r]) : 0.f;
+                    __builtin_fmaf(xv[r], scs[r], bis[r]) > 0.f ? round_bf16(v[r]) : 0.f;
                 dv[r] = d;
                 s1[a][r] += d;
-                s2[a][r] += d * (xv[r] - sh[a][r]);
+                s2[a][r] += d * (xv[r] - mus[r]);
               }
               *reinterpret_cast<u32x2*>(Y + row * g.K + col) =
                   u32x2{cvt_pk_bf16(dv[0], dv[1]), cvt_pk_bf16(dv[2], dv[3])};

@@ -178,10 +178,11 @@ def conv1x1_stats(m: nn.Conv2d, x: torch.Tensor, shift):
 
 
 # ---------------------------------------------------------------- 3x3 implicit GEMM
-# bench.py A/B (1 box, 2 runs each): data gradient on MIOpen 13,219-13,238 img/s, on mivod
-# for <= 64 / <= 128 channels 13,129-13,132 / 13,040-13,091, always 12,809-12,869: the
-# BN-reduce epilogue variant is not yet ahead in the full step, so MIOpen keeps it
-_DGRAD_DEFAULT = "0"
+# scripts/micro_dgrad_bn.py (dgrad + BN1 backward, MIOpen vs mivod with the BN reduce in
+# the epilogue): layer1 1858 -> 1654 us, layer2 1145 -> 1034 us, layer3 714 -> 743 us,
+# layer4 633 -> 625 us; so mivod takes the <= 128-channel data gradients.  (Before the
+# EPI-2 variant's register diet it ran one workgroup per CU and lost in the full step.)
+_DGRAD_DEFAULT = "128"
 
 
 def conv3x3_eligible(m: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -291,6 +292,7 @@ def bwd3x3_fusable(m: nn.Conv2d, x: torch.Tensor):
     slot = getattr(x, "_mv_slot", None)
     if (slot is None or getattr(slot, "bn", None) is None or getattr(slot, "mode", 0) != 1
             or os.environ.get("MIVOD_CONV_BN_BWD_FUSE", "1") == "0"
+            or os.environ.get("MIVOD_CONV3X3_BN_BWD", "1") == "0"
             or not (torch.is_grad_enabled() and x.requires_grad) or m.stride[0] != 1
             or not _dgrad_on_mivod(m.in_channels, m.out_channels)):
         return None
