@@ -1041,6 +1041,31 @@ at::Tensor wgrad3x3(at::Tensor x, at::Tensor dy, int64_t stride) {
   return dw;
 }
 
+// weight gradient of y = conv1x1(x, w, stride, pad 0): dw [K, C, 1, 1] bf16
+at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "wgrad1x1: x must be a channels_last bf16 GPU tensor");
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.device() == x.device(),
+              "wgrad1x1: dy must be a channels_last bf16 tensor on x's device");
+  TORCH_CHECK(stride == 1 || stride == 2, "wgrad1x1: stride must be 1 or 2");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == Ho && dy.size(3) == Wo, "wgrad1x1: dy shape");
+  TORCH_CHECK(C % 64 == 0 && K % 64 == 0 && N * H * W * std::max(C, K) < (int64_t(1) << 40),
+              "wgrad1x1: channels must be multiples of 64");
+  c10::DeviceGuard guard(x.device());
+  const int64_t M = N * Ho * Wo;
+  at::Tensor work = at::empty({mv_wgrad1x1_workspace(M, (int)K, (int)C)},
+                              x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({K, C, 1, 1}, x.options(), at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(mv_wgrad1x1(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), work.data_ptr<float>(),
+                          (int)N, (int)H, (int)W, (int)C, (int)K, (int)stride, cur_stream()),
+              "wgrad1x1: unsupported shape");
+  return dw;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_mvk, m) {
@@ -1100,6 +1125,8 @@ PYBIND11_MODULE(_mvk, m) {
         py::arg("partial") = py::none());
   m.def("conv3x3_bn_bwd", &conv3x3_bn_bwd,
         "stride-1 3x3 data gradient with the producing BN+ReLU's backward reduce fused");
+  m.def("wgrad1x1", &wgrad1x1, "1x1 (pad 0, stride 1/2) conv weight gradient on MFMA",
+        py::arg("x"), py::arg("dy"), py::arg("stride") = 1);
   m.def("wgrad3x3", &wgrad3x3, "3x3 (pad 1) conv weight gradient on MFMA (transposed LDS reads)",
         py::arg("x"), py::arg("dy"), py::arg("stride") = 1);
   m.def("conv3x3_partials", &conv3x3_partials, "partial rows of conv3x3's statistics epilogue");

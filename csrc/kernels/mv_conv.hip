@@ -641,3 +641,280 @@ bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, in
                      (const float*)work, (__bf16*)dw, K, C, ms);
   return true;
 }
+
+// ===========================================================================
+// 1x1 weight gradient (pad 0, stride 1 / 2):  dW[k][c] = sum_m dy[m][k] . X[pix(m)][c]
+// (pix(m) = m at stride 1; the strided input pixel of output pixel m at stride 2).
+// A dy^T . X GEMM reduced over the N*Ho*Wo output pixels: each wave owns a 64(k) x
+// 64(c) accumulator block; a workgroup's 4 waves are laid out WK x WC over a
+// (64 WK) x (64 WC) output tile and WS ways over the m rows of a stage (WS > 1 only for
+// the 64-channel tiles, so every workgroup still runs 4 waves), and a workgroup walks
+// a contiguous range of stages.  Staging as wgrad3x3: per stage WS x (WK + WC) [32][64]
+// row-major sub-tiles via global_load_lds (one 16-B load per thread per sub-tile,
+// XOR-swizzled chunk), an NS-slot ring with counted vmcnt waits, both operands read
+// with ds_read_b64_tr_b16.  fp32 partials [msplit * WS][K][C] + a fixed-order reduce.
+// ===========================================================================
+namespace mv {
+namespace conv {
+
+template <int WK, int WC, int WS, int ST, int NS, int FK = 1>
+__global__ __launch_bounds__(WK * WC * WS * 64)
+__attribute__((amdgpu_waves_per_eu(FK == 2 ? 2 : 1))) void wgrad1x1_kernel(
+    const __bf16* __restrict__ X, const __bf16* __restrict__ DY, float* __restrict__ partial,
+    Geo g, int nkc, int msplit, int64_t nchunks) {
+  constexpr int NW = WK * WC * WS;
+  static_assert(NW == 4 || NW == 8, "four or eight waves per workgroup");
+  constexpr int KS = FK * WK;                  // dy sub-tiles (64 k each) per m slice
+  constexpr int SUB = KS + WC;                 // sub-tiles per m slice
+  constexpr int NSUB = WS * SUB;               // [32][64] sub-tiles per stage
+  constexpr int HPW = NW / 4;                  // 256-thread groups (one sub-tile each)
+  static_assert(NSUB % HPW == 0, "sub-tiles split evenly over the thread groups");
+  constexpr int LPS = NSUB / HPW;              // glds per thread per stage
+  constexpr int ROWS = 32 * WS;                // m rows per stage
+  constexpr int STAGE = NSUB * WG_TILE;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t = remap(blockIdx.x, gridDim.x);
+  const int kc = t % nkc, ms = t / nkc;
+  const int cblocks = g.C / (64 * WC);
+  const int k0 = (kc / cblocks) * (64 * KS), c0 = (kc % cblocks) * (64 * WC);
+  const int64_t per = (nchunks + msplit - 1) / msplit;
+  const int64_t ch0 = ms * per;
+  const int64_t ch1 = ch0 + per < nchunks ? ch0 + per : nchunks;
+
+  // staging role: thread group h = tid >> 8 loads sub-tiles h, h + HPW, ...; within a
+  // sub-tile, row l >> 3 and (swizzled) 16-byte chunk of l = tid & 255
+  const int hg = HPW == 1 ? 0 : tid >> 8, l = tid & 255;
+  const int srow = l >> 3, sch = (l & 7) ^ wswz(l >> 3);
+  const uint64_t zaddr = (uint64_t)(g_zero + (l & 7) * 4);
+  const uint32_t hw = (uint32_t)(g.Ho * g.Wo);
+  auto issue = [&](int64_t chk, int slot) {
+    __bf16* stg = smem + slot * STAGE + (l - lane) * 8;     // + this wave's 1 KB of a sub-tile
+    int64_t mrow[WS], xrow[WS];
+#pragma unroll
+    for (int ws = 0; ws < WS; ++ws) {
+      const int64_t m = chk * ROWS + ws * 32 + srow;
+      mrow[ws] = m;
+      xrow[ws] = m;
+      if (ST == 2 && m < g.M) {
+        const uint32_t mm = (uint32_t)m, n = mm / hw, rem = mm - n * hw;
+        const uint32_t ho = rem / (uint32_t)g.Wo, wo = rem - ho * (uint32_t)g.Wo;
+        xrow[ws] = ((int64_t)n * g.H + 2 * ho) * g.W + 2 * wo;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < LPS; ++i) {
+      const int j = i * HPW + hg;                 // sub-tile (thread-group uniform)
+      const int ws = WS == 1 ? 0 : j / SUB, r = j % SUB;
+      const bool in = mrow[ws] < g.M;
+      const void* src = r < KS ? (const void*)(DY + mrow[ws] * g.K + k0 + r * 64 + sch * 8)
+                               : (const void*)(X + xrow[ws] * g.C + c0 + (r - KS) * 64 + sch * 8);
+      glds16(in ? src : (const void*)zaddr, stg + j * WG_TILE);
+    }
+  };
+
+  // wave role: m slice wsw, k block wkw, c block wcw
+  const int wcw = wid % WC, wkw = (wid / WC) % WK, wsw = wid / (WC * WK);
+  const int gq = lane >> 4, cl = lane & 15;
+  f32x4v acc[4 * FK][4];
+#pragma unroll
+  for (int u = 0; u < 4 * FK; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) acc[u][v] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  if (ch0 < ch1) {
+    // lookahead NS - 1 stages: stage chk + NS - 1 is issued right after the barrier that
+    // retires stage chk - 1 (the slot it reuses)
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+      if (ch0 + p < ch1) issue(ch0 + p, p);
+    int slot = 0;
+    for (int64_t chk = ch0; chk < ch1; ++chk) {
+      if (NS == 3 && chk + 1 < ch1)
+        wait_vm<LPS>();
+      else
+        wait_vm<0>();
+      raw_barrier();
+      if (chk + NS - 1 < ch1) issue(chk + NS - 1, slot == 0 ? NS - 1 : slot - 1);
+      const __bf16* st = smem + slot * STAGE;
+      const __bf16* ta = st + (wsw * SUB + wkw * FK) * WG_TILE;
+      const __bf16* tb = st + (wsw * SUB + KS + wcw) * WG_TILE;
+      bf16x8 af[4 * FK], bfr[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) bfr[v] = tr8(tb, 8 * gq, 8 * gq + 4, 16 * v, cl);
+#pragma unroll
+      for (int u = 0; u < 4 * FK; ++u)
+        af[u] = tr8(ta + (u >> 2) * WG_TILE, 8 * gq, 8 * gq + 4, 16 * (u & 3), cl);
+#pragma unroll
+      for (int u = 0; u < 4 * FK; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[u][v] = mfma(af[u], bfr[v], acc[u][v]);
+      slot = slot == NS - 1 ? 0 : slot + 1;
+    }
+    wait_vm<0>();
+  }
+  // partial[ms * WS + wsw][k][c]; written even with no chunks (zeros)
+  float* pb = partial + ((int64_t)ms * WS + wsw) * g.K * g.C;
+#pragma unroll
+  for (int u = 0; u < 4 * FK; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + wkw * FK * 64 + 16 * u + 4 * gq + r, c = c0 + wcw * 64 + 16 * v + cl;
+        pb[(int64_t)k * g.C + c] = acc[u][v][r];
+      }
+}
+
+// dw[e] (bf16) = sum_p partial[p][e], fixed order: PS lanes split the P slices, then one
+// lane sums the PS lane totals in lane order
+template <int PS>
+__global__ __launch_bounds__(256) void wgrad1x1_reduce_kernel(const float* __restrict__ partial,
+                                                               __bf16* __restrict__ dw, int64_t E,
+                                                               int P) {
+  constexpr int COLS = 256 / PS;
+  __shared__ float4 red[PS][COLS];
+  const int q = threadIdx.x % COLS, p = threadIdx.x / COLS;
+  const int64_t i4 = (int64_t)blockIdx.x * COLS + q;
+  const bool ok = i4 * 4 < E;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok)
+    for (int pp = p; pp < P; pp += PS) {
+      const float4 v = reinterpret_cast<const float4*>(partial + (int64_t)pp * E)[i4];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+  red[p][q] = s;
+  __syncthreads();
+  if (p == 0 && ok) {
+    float4 a = red[0][q];
+    for (int j = 1; j < PS; ++j) {
+      const float4 b = red[j][q];
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    __bf16* o = dw + i4 * 4;
+    o[0] = (__bf16)a.x;
+    o[1] = (__bf16)a.y;
+    o[2] = (__bf16)a.z;
+    o[3] = (__bf16)a.w;
+  }
+}
+
+}  // namespace conv
+}  // namespace mv
+
+namespace {
+struct W1Cfg {
+  int wk, wc, ws, ns, fk = 1;
+};
+// tile layout per shape (scripts/micro_wgrad1x1.py sweeps): 128x128 tiles on a 2-slot ring
+// (4 workgroups per CU) once there are >= 8 tiles, else a 3-slot ring (3 per CU) — fewer
+// tiles mean more m splits and the 64 MB of partials of a full grid start to show;
+// 64-channel shapes split the m rows of a stage over the waves
+W1Cfg w1_cfg(int K, int C) {
+  const char* fk = std::getenv("MIVOD_WGRAD1_FK");
+  if (fk && std::atoi(fk) == 2 && K % 256 == 0 && C % 128 == 0) return {2, 2, 1, 3, 2};
+  const char* wv = std::getenv("MIVOD_WGRAD1_WAVES");
+  if (wv && std::atoi(wv) == 8) {
+    if (K % 256 == 0 && C % 128 == 0) return {4, 2, 1, 3};
+    if (K % 128 == 0 && C % 256 == 0) return {2, 4, 1, 3};
+  }
+  if (K % 128 == 0 && C % 128 == 0) {
+    const char* e = std::getenv("MIVOD_WGRAD1_NS");     // ring depth A/B for the 128x128 tile
+    const int ntiles = (K / 128) * (C / 128);
+    const int ns = e && std::atoi(e) > 0 ? std::atoi(e) : (ntiles >= 8 ? 2 : 3);
+    return {2, 2, 1, ns == 2 ? 2 : 3};
+  }
+  if (K % 128 == 0) return {2, 1, 2, 2};
+  if (C % 128 == 0) return {1, 2, 2, 2};
+  return {1, 1, 4, 2};
+}
+int w1_msplit(int64_t nchunks, int ntiles, const W1Cfg& c) {
+  const char* e = std::getenv("MIVOD_WGRAD1_BLOCKS");
+  const int nw = c.wk * c.wc * c.ws;
+  const int64_t target = e && std::atoi(e) > 0 ? std::atoi(e)
+                         : (nw == 8 || c.fk == 2) ? 512
+                         : (c.ns == 3 ? 768 : (c.wk == 2 && c.wc == 2 ? 1024 : 512));
+  int64_t ms = target / ntiles;
+  if (ms < 1) ms = 1;
+  if (ms > nchunks) ms = nchunks;
+  return (int)ms;
+}
+}  // namespace
+
+int64_t mv_wgrad1x1_workspace(int64_t M, int K, int C) {
+  const W1Cfg c = w1_cfg(K, C);
+  const int ntiles = (K / (64 * c.wk * c.fk)) * (C / (64 * c.wc));
+  const int64_t nchunks = (M + 32 * c.ws - 1) / (32 * c.ws);
+  return (int64_t)w1_msplit(nchunks, ntiles, c) * c.ws * K * C;
+}
+
+bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
+                 int K, int stride, hipStream_t st) {
+  using namespace mv::conv;
+  if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2)) return false;
+  Geo g;
+  g.H = H;
+  g.W = W;
+  g.C = C;
+  g.K = K;
+  g.st = stride;
+  g.ks = 1;
+  g.Ho = (H - 1) / stride + 1;
+  g.Wo = (W - 1) / stride + 1;
+  g.M = (int64_t)N * g.Ho * g.Wo;
+  if (stride == 2 && g.M >= (int64_t(1) << 32)) return false;
+  const W1Cfg c = w1_cfg(K, C);
+  const int ntiles = (K / (64 * c.wk * c.fk)) * (C / (64 * c.wc));
+  const int64_t nchunks = (g.M + 32 * c.ws - 1) / (32 * c.ws);
+  const int ms = w1_msplit(nchunks, ntiles, c);
+  const dim3 grid((unsigned)(ntiles * ms)), blk((unsigned)(64 * c.wk * c.wc * c.ws));
+  const __bf16 *xp = (const __bf16*)x, *dp = (const __bf16*)dy;
+#define MV_W1F(WKV, WCV, WSV, NSV, FKV)                                                       \
+  if (stride == 1)                                                                           \
+    hipLaunchKernelGGL((wgrad1x1_kernel<WKV, WCV, WSV, 1, NSV, FKV>), grid, blk, 0, st, xp, dp,  \
+                       work, g, ntiles, ms, nchunks);                                        \
+  else                                                                                       \
+    hipLaunchKernelGGL((wgrad1x1_kernel<WKV, WCV, WSV, 2, NSV, FKV>), grid, blk, 0, st, xp, dp,  \
+                       work, g, ntiles, ms, nchunks);
+#define MV_W1(WKV, WCV, WSV, NSV) MV_W1F(WKV, WCV, WSV, NSV, 1)
+  if (c.fk == 2) {
+    MV_W1F(2, 2, 1, 3, 2)
+  } else if (c.wk == 4) {
+    MV_W1(4, 2, 1, 3)
+  } else if (c.wc == 4) {
+    MV_W1(2, 4, 1, 3)
+  } else if (c.wk == 2 && c.wc == 2) {
+    if (c.ns == 3) {
+      MV_W1(2, 2, 1, 3)
+    } else {
+      MV_W1(2, 2, 1, 2)
+    }
+  } else if (c.wk == 2) {
+    MV_W1(2, 1, 2, 2)
+  } else if (c.wc == 2) {
+    MV_W1(1, 2, 2, 2)
+  } else {
+    MV_W1(1, 1, 4, 2)
+  }
+#undef MV_W1
+#undef MV_W1F
+  const int P = ms * c.ws;
+  const int64_t E = (int64_t)K * C;
+  if (P >= 64)
+    hipLaunchKernelGGL((wgrad1x1_reduce_kernel<64>), dim3((unsigned)((E / 4 + 3) / 4)), dim3(256),
+                       0, st, (const float*)work, (__bf16*)dw, E, P);
+  else if (P >= 16)
+    hipLaunchKernelGGL((wgrad1x1_reduce_kernel<16>), dim3((unsigned)((E / 4 + 15) / 16)),
+                       dim3(256), 0, st, (const float*)work, (__bf16*)dw, E, P);
+  else
+    hipLaunchKernelGGL((wgrad1x1_reduce_kernel<4>), dim3((unsigned)((E / 4 + 63) / 64)), dim3(256),
+                       0, st, (const float*)work, (__bf16*)dw, E, P);
+  return true;
+}

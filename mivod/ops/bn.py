@@ -95,7 +95,8 @@ class _Tap(torch.autograd.Function):
 
 class _DownsampleTapConv(torch.autograd.Function):
     """Shortcut ``conv1x1(x, stride=s)`` of a tapped output (ResNet stage entry).
-    Backward: dW from the backward-weights solver; the input gradient is computed
+    Backward: dW from ops.conv.wgrad1x1 (mivod's kernel from 128 channels, else the
+    backward-weights solver); the input gradient is computed
     at the OUTPUT resolution as a forward 1x1 conv with the transposed filter and
     parked in x's producer slot with ``stride = s`` — the producer's BN backward
     kernel adds it on the stride grid.  No full-resolution zero-filled gradient
@@ -119,9 +120,8 @@ class _DownsampleTapConv(torch.autograd.Function):
             ctx.slot.stride = ctx.s
             ctx.slot.full_shape = x.shape
         if ctx.needs_input_grad[1]:
-            _, dw, _ = torch.ops.aten.convolution_backward(
-                dy, x, w, None, [ctx.s, ctx.s], [0, 0], [1, 1], False, [0, 0], 1,
-                [False, True, False])
+            from .conv import wgrad1x1
+            dw = wgrad1x1(dy, x, w, ctx.s)
         return None, dw, None, None
 
 

@@ -44,6 +44,27 @@ def _transposed_filter(w: torch.Tensor) -> torch.Tensor:
     return wt.contiguous(memory_format=torch.channels_last)
 
 
+def _wgrad1x1_on_mivod(cin: int, cout: int) -> bool:
+    """mivod's 1x1 weight-gradient kernel (csrc/kernels/mv_conv.hip wgrad1x1_kernel) vs
+    MIOpen's backward-weights solver on the ResNet-50 bs2048 shapes (scripts/
+    micro_wgrad1x1.py, profiles/r2_wgrad1x1_vs_miopen.txt): level on the HBM-bound
+    64-channel ones (kept on MIOpen), 3-23% faster from 128 channels up."""
+    return (os.environ.get("MIVOD_WGRAD1X1", "1") != "0" and min(cin, cout) >= 128
+            and cin % 64 == 0 and cout % 64 == 0)
+
+
+def wgrad1x1(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int = 1) -> torch.Tensor:
+    """dW of y = conv1x1(x, w, stride, pad 0) — mivod's kernel where it wins, else MIOpen."""
+    if (_wgrad1x1_on_mivod(w.shape[1], w.shape[0]) and x.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and dy.is_contiguous(memory_format=torch.channels_last)):
+        from . import kernels as K
+        return K.native().wgrad1x1(x, dy, stride)
+    _, dw, _ = torch.ops.aten.convolution_backward(
+        dy, x, w, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])
+    return dw
+
+
 class _ConvDgradFwd(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, pad):
@@ -59,9 +80,12 @@ class _ConvDgradFwd(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = F.conv2d(dy, _transposed_filter(w), None, 1, ctx.pad)
         if ctx.needs_input_grad[1]:
-            _, dw, _ = torch.ops.aten.convolution_backward(
-                dy, x, w, None, [1, 1], [ctx.pad, ctx.pad], [1, 1], False, [0, 0], 1,
-                [False, True, False])
+            if w.shape[2] == 1 and w.shape[3] == 1:
+                dw = wgrad1x1(dy, x, w)
+            else:
+                _, dw, _ = torch.ops.aten.convolution_backward(
+                    dy, x, w, None, [1, 1], [ctx.pad, ctx.pad], [1, 1], False, [0, 0], 1,
+                    [False, True, False])
         return dx, dw, None
 
 
@@ -139,8 +163,7 @@ class _Conv1x1BN(torch.autograd.Function):
             else:
                 dx = F.conv2d(dy, _transposed_filter(w))
         if ctx.needs_input_grad[1]:
-            _, dw, _ = torch.ops.aten.convolution_backward(
-                dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])
+            dw = wgrad1x1(dy, x, w)
         return dx, dw, None, None, None
 
 

@@ -164,6 +164,50 @@ def test_wgrad3x3_matches_fp32(cuda, n, c, k, h, w, s):
     torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
 
 
+@pytest.mark.parametrize("n,c,k,h,w,s", [(2, 128, 256, 9, 7, 1), (3, 256, 128, 10, 10, 2),
+                                         (2, 64, 256, 8, 9, 1), (2, 256, 64, 7, 7, 1),
+                                         (3, 64, 64, 11, 5, 1), (2, 512, 1024, 7, 7, 2),
+                                         (1, 64, 128, 3, 3, 2)])
+def test_wgrad1x1_matches_fp32(cuda, n, c, k, h, w, s):
+    """All four tile layouts (128x128, 128x64 / 64x128 with 2 m slices, 64x64 with 4),
+    stride 1 and 2 (odd sizes), m tails that are not multiples of the stage rows."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(n + c + k + h + s)
+    x = _cl(torch.randn(n, c, h, w, device=cuda, generator=g).to(torch.bfloat16))
+    ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+    dy = _cl(torch.randn(n, k, ho, wo, device=cuda, generator=g).to(torch.bfloat16))
+    wref = torch.zeros(k, c, 1, 1, device=cuda, requires_grad=True)
+    F.conv2d(x.float(), wref, None, s).backward(dy.float())
+    dw = nat.wgrad1x1(x, dy, s)
+    assert dw.shape == (k, c, 1, 1)
+    ref = wref.grad
+    torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
+    assert torch.equal(nat.wgrad1x1(x, dy, s), dw)          # fixed-order reduce
+
+
+def test_resnet_uses_wgrad1x1(cuda, monkeypatch):
+    """The ResNet bottlenecks' >= 128-channel 1x1 weight gradients (conv1 / conv3 of the
+    fused conv+BN path, plain stride-1 1x1 convs and the strided downsample shortcut) run
+    on mivod's wgrad1x1 kernel."""
+    from mivod.models.resnet import ResNet, to_mixed_bf16
+    nat = _nat()
+    calls = []
+    real = nat.wgrad1x1
+
+    def counted(x, dy, s=1):
+        calls.append((x.shape[1], dy.shape[1], s))
+        return real(x, dy, s)
+
+    monkeypatch.setattr(nat, "wgrad1x1", counted)
+    torch.manual_seed(0)
+    m = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
+    x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
+    F.cross_entropy(m(x).float(), torch.randint(0, 10, (4,), device=cuda)).backward()
+    assert any(s == 2 for _, _, s in calls), calls          # stage-entry shortcut
+    assert all(min(c, k) >= 128 for c, k, _ in calls), calls
+    assert len(calls) >= 10, calls
+
+
 @pytest.mark.parametrize("n,c,k,h,w,s", [(2, 512, 128, 9, 7, 1), (3, 1024, 256, 7, 7, 1),
                                          (2, 256, 512, 10, 10, 2), (1, 64, 64, 5, 6, 1)])
 def test_conv1x1_kernel_matches_fp32(cuda, n, c, k, h, w, s):
