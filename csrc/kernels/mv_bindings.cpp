@@ -983,16 +983,18 @@ at::Tensor conv_nhwc(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<a
 
 // data gradient of a stride-1 3x3 conv (dy . flipped filter) with the mode-1 (BN+ReLU)
 // backward reduce of the BN that produced the conv's input fused into the epilogue:
-// returns (d = relu'(x_bn) * dgrad, partials [P, 2, C])
+// returns (d = relu'(x_bn) * dgrad, partials [P, 2, C]).  Also the stride-1 1x1 conv
+// (wt [C, K, 1, 1]): the same kernel with ks = 1.
 std::vector<at::Tensor> conv3x3_bn_bwd(at::Tensor dy, at::Tensor wt, at::Tensor x_bn,
                                        at::Tensor vec) {
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
                   dy.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv3x3_bn_bwd: dy must be a channels_last bf16 GPU tensor");
   TORCH_CHECK(wt.is_cuda() && wt.scalar_type() == at::kBFloat16 && wt.dim() == 4 &&
-                  wt.size(2) == 3 && wt.size(3) == 3 && wt.size(1) == dy.size(1) &&
-                  wt.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "conv3x3_bn_bwd: wt must be the channels_last [C, K, 3, 3] transposed filter");
+                  wt.size(2) == wt.size(3) && (wt.size(2) == 3 || wt.size(2) == 1) &&
+                  wt.size(1) == dy.size(1) && wt.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_bn_bwd: wt must be the channels_last [C, K, ks, ks] (ks 3 or 1) "
+              "transposed filter");
   const int64_t N = dy.size(0), K = dy.size(1), H = dy.size(2), W = dy.size(3), C = wt.size(0);
   TORCH_CHECK(C % 64 == 0 && K % 64 == 0, "conv3x3_bn_bwd: channels must be multiples of 64");
   TORCH_CHECK(x_bn.is_cuda() && x_bn.scalar_type() == at::kBFloat16 &&
@@ -1009,9 +1011,9 @@ std::vector<at::Tensor> conv3x3_bn_bwd(at::Tensor dy, at::Tensor wt, at::Tensor 
   const int64_t M = N * H * W;
   at::Tensor d = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
   at::Tensor part = at::empty({conv3x3_partials(M, C), 2, C}, dy.options().dtype(at::kFloat));
-  TORCH_CHECK(mv_conv3x3(dy.data_ptr(), wt.data_ptr(), d.data_ptr(), (int)N, (int)H, (int)W, (int)K,
-                         (int)C, 1, nullptr, part.data_ptr<float>(), cur_stream(), x_bn.data_ptr(),
-                         vec.data_ptr<float>()),
+  TORCH_CHECK(mv_conv_nhwc(dy.data_ptr(), wt.data_ptr(), d.data_ptr(), (int)N, (int)H, (int)W,
+                           (int)K, (int)C, (int)wt.size(2), 1, nullptr, part.data_ptr<float>(),
+                           cur_stream(), x_bn.data_ptr(), vec.data_ptr<float>()),
               "conv3x3_bn_bwd: unsupported shape");
   return {d, part};
 }

@@ -50,3 +50,27 @@ for h, c in ((56, 64), (28, 128), (14, 256), (7, 512)):
           f"{t_ep + t_fin:7.1f} us", flush=True)
     del dy, xb, g, d
     torch.cuda.empty_cache()
+
+# ---- bottleneck conv3 (1x1, 4c -> c data gradient) + BN2 (BN+ReLU) backward: the unfused
+# path (mivod streaming GEMM for 4c = 256, MIOpen's forward solver otherwise) vs the
+# implicit-GEMM kernel with ks = 1 and the reduce epilogue
+for h, c in ((56, 64), (28, 128), (14, 256), (7, 512)):
+    cl = torch.channels_last
+    dy = torch.randn(BS, 4 * c, h, h, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (torch.randn(4 * c, c, 1, 1, device=dev) / c ** 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    wt = w.transpose(0, 1).contiguous(memory_format=cl)
+    xb = torch.randn(BS, c, h, h, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    gm = torch.ones(c, device=dev)
+    _, vec = nat.bn_fwd_train(xb, gm, torch.zeros(c, device=dev), torch.zeros(c, device=dev),
+                              torch.ones(c, device=dev), 0.1, 1e-5, True, None)
+    t_mi = tm(lambda: F.conv2d(dy, wt))
+    g = F.conv2d(dy, wt)
+    t_bn = tm(lambda: nat.bn_bwd(1, g, xb, None, vec, gm, True, None, 1))
+    t_ep = tm(lambda: nat.conv3x3_bn_bwd(dy, wt, xb, vec))
+    d, part = nat.conv3x3_bn_bwd(dy, wt, xb, vec)
+    t_fin = tm(lambda: nat.bn_bwd_from_partials(d, xb, vec, gm, True, part))
+    print(f"1x1 H{h:3d} {4 * c:4d}->{c:4d}: MIOpen dgrad {t_mi:7.1f} + bn_bwd {t_bn:7.1f} = "
+          f"{t_mi + t_bn:7.1f} us | fused dgrad+reduce {t_ep:7.1f} + finalize/dx {t_fin:7.1f} = "
+          f"{t_ep + t_fin:7.1f} us", flush=True)
+    del dy, xb, g, d
+    torch.cuda.empty_cache()

@@ -105,19 +105,21 @@ def test_resnet_bottleneck_uses_conv3x3(cuda):
     assert any("Conv3x3" in n for n in names), names
 
 
-@pytest.mark.parametrize("c,k", [(64, 64), (128, 128), (64, 128)])
-def test_conv3x3_bn_bwd_matches_reference(cuda, c, k):
-    """dgrad (forward conv with the transposed filter) + mode-1 BN backward reduce in
-    the epilogue == conv2d + relu mask + (sum d, sum d (x - mean)) in fp32."""
+@pytest.mark.parametrize("c,k,ks", [(64, 64, 3), (128, 128, 3), (64, 128, 3), (64, 256, 1),
+                                    (128, 512, 1), (512, 2048, 1)])
+def test_conv3x3_bn_bwd_matches_reference(cuda, c, k, ks):
+    """dgrad (forward conv with the transposed filter; 3x3 or 1x1) + mode-1 BN backward
+    reduce in the epilogue == conv2d + relu mask + (sum d, sum d (x - mean)) in fp32."""
     nat = _nat()
     g = torch.Generator(device=cuda).manual_seed(c + 7 * k)
     n, h, w = 3, 11, 9
     dy = _cl(torch.randn(n, k, h, w, device=cuda, generator=g).to(torch.bfloat16))
-    wt = _cl((torch.randn(c, k, 3, 3, device=cuda, generator=g) / (9 * k) ** 0.5).to(torch.bfloat16))
+    wt = _cl((torch.randn(c, k, ks, ks, device=cuda, generator=g) / (ks * ks * k) ** 0.5).to(
+        torch.bfloat16))
     xb = _cl(torch.randn(n, c, h, w, device=cuda, generator=g).to(torch.bfloat16))
     vec = torch.randn(4, c, device=cuda, generator=g)
     d, part = nat.conv3x3_bn_bwd(dy, wt, xb, vec)
-    dg = F.conv2d(dy.float(), wt.float(), None, 1, 1).to(torch.bfloat16).float()
+    dg = F.conv2d(dy.float(), wt.float(), None, 1, ks // 2).to(torch.bfloat16).float()
     on = (xb.float() * vec[2].view(1, -1, 1, 1) + vec[3].view(1, -1, 1, 1)) > 0
     ref = torch.where(on, dg, torch.zeros_like(dg))
     torch.testing.assert_close(d.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
@@ -136,16 +138,18 @@ def test_resnet_uses_conv3x3_bwd_fusion(cuda, monkeypatch):
     real = nat.conv3x3_bn_bwd
 
     def counted(*a):
-        calls.append(a[0].shape)
+        calls.append(a[1].shape[2])
         return real(*a)
 
     monkeypatch.setattr(nat, "conv3x3_bn_bwd", counted)
-    monkeypatch.setenv("MIVOD_CONV3X3_DGRAD", "1")     # off by default (bench A/B)
+    monkeypatch.setenv("MIVOD_CONV3X3_DGRAD", "1")     # every width (default: <= 128)
+    monkeypatch.setenv("MIVOD_CONV1X1_BN_BWD", "1")    # opt-in (bench A/B neutral)
     torch.manual_seed(0)
     m = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
     x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
     F.cross_entropy(m(x).float(), torch.randint(0, 10, (4,), device=cuda)).backward()
-    assert len(calls) == 4, calls       # layer1.0, layer1.1, layer2.1, layer3.1 (x.0: stride 2)
+    # 3x3: layer1.0, layer1.1, layer2.1, layer3.1 (x.0: stride 2); 1x1: every conv3 (BN2)
+    assert calls.count(3) == 4 and calls.count(1) == 7, calls
 
 
 @pytest.mark.parametrize("n,c,k,h,w,s", [(2, 64, 64, 9, 7, 1), (3, 128, 128, 10, 10, 2),
