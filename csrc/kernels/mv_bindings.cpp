@@ -837,9 +837,14 @@ int64_t gemm_bwd_partials(int64_t M, int64_t N, int64_t K, int64_t bn) {
 // Data-gradient GEMM of a 1x1 conv fused with the BN+add+ReLU (mode 3) backward
 // reduce of the BN that produced the conv's input: dy = a . b^T, dz = mask ? dy + dy2
 // : 0 is written to dz, returns the fp32 [P, 2, N] partials (sum dz, sum dz (x - mean)).
+// x = None: only sum dz (the second partial is 0; ops.bn._Conv1x1BNFold gets it from its
+// weight-gradient GEMM) and the BN input is never read.
 at::Tensor gemm_nt_bn_bwd(at::Tensor a, at::Tensor b, at::Tensor dz,
-                          c10::optional<at::Tensor> dy2, at::Tensor mask, at::Tensor x,
-                          at::Tensor vec, int64_t bn, int64_t dy2_stride, int64_t H, int64_t W) {
+                          c10::optional<at::Tensor> dy2, at::Tensor mask,
+                          c10::optional<at::Tensor> xo, at::Tensor vec, int64_t bn,
+                          int64_t dy2_stride, int64_t H, int64_t W) {
+  const bool has_x = xo.has_value() && xo->defined();
+  at::Tensor x = has_x ? *xo : dz;
   for (const at::Tensor* t : {&a, &b, &dz, &x})
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous(),
                 "gemm_nt_bn_bwd: A, B, dz, x must be contiguous bf16 GPU tensors");
@@ -881,11 +886,37 @@ at::Tensor gemm_nt_bn_bwd(at::Tensor a, at::Tensor b, at::Tensor dz,
   c10::DeviceGuard guard(a.device());
   at::Tensor partial = at::empty({P, 2, N}, a.options().dtype(at::kFloat));
   TORCH_CHECK(mv_gemm_nt_bn_bwd(a.data_ptr(), b.data_ptr(), dz.data_ptr(), M, (int)N, (int)K, d2,
-                                mask.data_ptr(), x.data_ptr(), vec[0].data_ptr<float>(),
+                                mask.data_ptr(), has_x ? x.data_ptr() : nullptr,
+                                vec[0].data_ptr<float>(),
                                 partial.data_ptr<float>(), (int)bn, cur_stream(), (int)dy2_stride,
                                 (int)H, (int)W),
               "gemm_nt_bn_bwd: launch failed");
   return partial;
+}
+
+// [5, C] fp32 = (dgamma, dbeta, ca, cb, cc) from a GEMM-epilogue reduce's partials, with
+// the BN's input gradient dx = ca * dz + cb * x + cc (per channel) left to the caller
+at::Tensor bn_bwd_coeffs(at::Tensor vec, c10::optional<at::Tensor> gamma, at::Tensor partial,
+                         int64_t M) {
+  TORCH_CHECK(partial.is_cuda() && partial.scalar_type() == at::kFloat && partial.is_contiguous() &&
+                  partial.dim() == 3 && partial.size(1) == 2 && partial.size(0) > 0 &&
+                  partial.size(0) < (int64_t(1) << 31),
+              "bn: partials must be fp32 [P, 2, C]");
+  const int64_t C = partial.size(2);
+  TORCH_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() &&
+              vec.numel() == 4 * C && vec.device() == partial.device(),
+              "bn: saved stats must be fp32 [4, C]");
+  TORCH_CHECK(M > 0, "bn: M must be positive");
+  c10::DeviceGuard guard(vec.device());
+  at::Tensor work = at::empty({5, C}, vec.options());
+  mv_bn_bwd_from_partials(nullptr, nullptr, nullptr, M, (int)C, vec[0].data_ptr<float>(),
+                          vec[1].data_ptr<float>(), opt_f32(gamma, C, "weight"),
+                          vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
+                          work[0].data_ptr<float>(), work[1].data_ptr<float>(),
+                          partial.data_ptr<float>(), (int)partial.size(0),
+                          work[2].data_ptr<float>(), work[3].data_ptr<float>(),
+                          work[4].data_ptr<float>(), cur_stream());
+  return work;
 }
 
 // {dx, dgamma, dbeta} from a GEMM-epilogue reduce (gemm_nt_bn_bwd)
@@ -1044,7 +1075,7 @@ at::Tensor wgrad3x3(at::Tensor x, at::Tensor dy, int64_t stride) {
 }
 
 // weight gradient of y = conv1x1(x, w, stride, pad 0): dw [K, C, 1, 1] bf16
-at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride) {
+at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride, bool fp32_out) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "wgrad1x1: x must be a channels_last bf16 GPU tensor");
@@ -1061,9 +1092,11 @@ at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride) {
   const int64_t M = N * Ho * Wo;
   at::Tensor work = at::empty({mv_wgrad1x1_workspace(M, (int)K, (int)C)},
                               x.options().dtype(at::kFloat));
-  at::Tensor dw = at::empty({K, C, 1, 1}, x.options(), at::MemoryFormat::ChannelsLast);
+  at::Tensor dw = at::empty({K, C, 1, 1}, fp32_out ? x.options().dtype(at::kFloat) : x.options(),
+                            at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(mv_wgrad1x1(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), work.data_ptr<float>(),
-                          (int)N, (int)H, (int)W, (int)C, (int)K, (int)stride, cur_stream()),
+                          (int)N, (int)H, (int)W, (int)C, (int)K, (int)stride, cur_stream(),
+                          fp32_out),
               "wgrad1x1: unsupported shape");
   return dw;
 }
@@ -1117,6 +1150,8 @@ PYBIND11_MODULE(_mvk, m) {
         py::arg("W") = 1);
   m.def("gemm_bwd_partials", &gemm_bwd_partials, "partial rows of gemm_nt_bn_bwd (-1: unsupported)",
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bn") = 0);
+  m.def("bn_bwd_coeffs", &bn_bwd_coeffs,
+        "BN backward finalize only: [5, C] = (dgamma, dbeta, ca, cb, cc) from partials");
   m.def("bn_bwd_from_partials", &bn_bwd_from_partials,
         "BN backward finalize + dx from GEMM-epilogue partials -> (dx, dgamma, dbeta)");
   m.def("conv3x3", &conv3x3, "implicit-GEMM 3x3 conv (pad 1) with optional fused BN statistics",
@@ -1128,7 +1163,7 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("conv3x3_bn_bwd", &conv3x3_bn_bwd,
         "stride-1 3x3 data gradient with the producing BN+ReLU's backward reduce fused");
   m.def("wgrad1x1", &wgrad1x1, "1x1 (pad 0, stride 1/2) conv weight gradient on MFMA",
-        py::arg("x"), py::arg("dy"), py::arg("stride") = 1);
+        py::arg("x"), py::arg("dy"), py::arg("stride") = 1, py::arg("fp32_out") = false);
   m.def("wgrad3x3", &wgrad3x3, "3x3 (pad 1) conv weight gradient on MFMA (transposed LDS reads)",
         py::arg("x"), py::arg("dy"), py::arg("stride") = 1);
   m.def("conv3x3_partials", &conv3x3_partials, "partial rows of conv3x3's statistics epilogue");

@@ -757,6 +757,7 @@ void mv_bn_bwd_from_partials(const void* dz, const void* x, void* dx, int64_t M,
                              float* cb, float* cc, hipStream_t st) {
   hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
                      partial, P, M, C, save_mean, save_invstd, gamma, dgamma, dbeta, ca, cb, cc);
-  launch_bwd_dx<0>((const __bf16*)dz, (const __bf16*)x, scale, bias, ca, cb, cc, (__bf16*)dx, M, C,
-                   st);
+  if (dx)   // dx == nullptr: coefficients only (ops.conv._Conv1x1BNFold folds dx into its GEMMs)
+    launch_bwd_dx<0>((const __bf16*)dz, (const __bf16*)x, scale, bias, ca, cb, cc, (__bf16*)dx, M,
+                     C, st);
 }

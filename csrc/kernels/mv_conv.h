@@ -30,5 +30,6 @@ bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, in
 // 1x1 (pad 0, stride 1/2) weight gradient: dw[K, C] (bf16) of y = conv1x1(x, w, stride)
 // given dy; work: fp32 [mv_wgrad1x1_workspace(M, K, C)], M = N * Ho * Wo
 int64_t mv_wgrad1x1_workspace(int64_t M, int K, int C);
+// (dw_fp32: dw is fp32 instead of bf16)
 bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
-                 int K, int stride, hipStream_t st);
+                 int K, int stride, hipStream_t st, bool dw_fp32 = false);

@@ -769,9 +769,9 @@ __attribute__((amdgpu_waves_per_eu(FK == 2 ? 2 : 1))) void wgrad1x1_kernel(
 
 // dw[e] (bf16) = sum_p partial[p][e], fixed order: PS lanes split the P slices, then one
 // lane sums the PS lane totals in lane order
-template <int PS>
+template <int PS, typename TO>
 __global__ __launch_bounds__(256) void wgrad1x1_reduce_kernel(const float* __restrict__ partial,
-                                                               __bf16* __restrict__ dw, int64_t E,
+                                                               TO* __restrict__ dw, int64_t E,
                                                                int P) {
   constexpr int COLS = 256 / PS;
   __shared__ float4 red[PS][COLS];
@@ -798,11 +798,11 @@ __global__ __launch_bounds__(256) void wgrad1x1_reduce_kernel(const float* __res
       a.z += b.z;
       a.w += b.w;
     }
-    __bf16* o = dw + i4 * 4;
-    o[0] = (__bf16)a.x;
-    o[1] = (__bf16)a.y;
-    o[2] = (__bf16)a.z;
-    o[3] = (__bf16)a.w;
+    TO* o = dw + i4 * 4;
+    o[0] = (TO)a.x;
+    o[1] = (TO)a.y;
+    o[2] = (TO)a.z;
+    o[3] = (TO)a.w;
   }
 }
 
@@ -856,7 +856,7 @@ int64_t mv_wgrad1x1_workspace(int64_t M, int K, int C) {
 }
 
 bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
-                 int K, int stride, hipStream_t st) {
+                 int K, int stride, hipStream_t st, bool dw_fp32) {
   using namespace mv::conv;
   if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2)) return false;
   Geo g;
@@ -907,14 +907,26 @@ bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, in
 #undef MV_W1F
   const int P = ms * c.ws;
   const int64_t E = (int64_t)K * C;
-  if (P >= 64)
-    hipLaunchKernelGGL((wgrad1x1_reduce_kernel<64>), dim3((unsigned)((E / 4 + 3) / 4)), dim3(256),
-                       0, st, (const float*)work, (__bf16*)dw, E, P);
-  else if (P >= 16)
-    hipLaunchKernelGGL((wgrad1x1_reduce_kernel<16>), dim3((unsigned)((E / 4 + 15) / 16)),
-                       dim3(256), 0, st, (const float*)work, (__bf16*)dw, E, P);
-  else
-    hipLaunchKernelGGL((wgrad1x1_reduce_kernel<4>), dim3((unsigned)((E / 4 + 63) / 64)), dim3(256),
-                       0, st, (const float*)work, (__bf16*)dw, E, P);
+  const float* wk = work;
+#define MV_W1R(PSV, TO)                                                                        \
+  hipLaunchKernelGGL((wgrad1x1_reduce_kernel<PSV, TO>),                                        \
+                     dim3((unsigned)((E / 4 + 256 / PSV - 1) / (256 / PSV))), dim3(256), 0, st, wk, \
+                     (TO*)dw, E, P)
+  if (dw_fp32) {
+    if (P >= 64)
+      MV_W1R(64, float);
+    else if (P >= 16)
+      MV_W1R(16, float);
+    else
+      MV_W1R(4, float);
+  } else {
+    if (P >= 64)
+      MV_W1R(64, __bf16);
+    else if (P >= 16)
+      MV_W1R(16, __bf16);
+    else
+      MV_W1R(4, __bf16);
+  }
+#undef MV_W1R
   return true;
 }

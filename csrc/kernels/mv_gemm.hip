@@ -229,7 +229,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_nt_kernel(
 struct BwdEpi {
   const __bf16* dy2;      // [M, N] second gradient stream (shortcut), may be null
   const uint8_t* mask;    // [M, N/8] bitmask of the forward output > 0
-  const __bf16* x;        // [M, N] BN input
+  const __bf16* x;        // [M, N] BN input; null: only sum dz (second partial 0)
   const float* mean;      // [N] saved mean
   // ds > 1: dy2 lives on the stride-ds grid of the [*, H, W] rows (the input gradient
   // of a strided 1x1 shortcut conv, ops/bn.py downsample_tap): row (n, h, w) adds
@@ -338,7 +338,12 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
             for (int j = 0; j < NC / 2; ++j) e2[b][j] = 0u;
           }
         }
-        ld_raw<NC>(be.x + row * N + cbase, ex[b]);
+        if (be.x) {
+          ld_raw<NC>(be.x + row * N + cbase, ex[b]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < NC / 2; ++j) ex[b][j] = 0u;
+        }
         const uint8_t* mp = be.mask + row * (N / 8) + cbase / 8;
         if constexpr (NC == 4) em[b] = (uint32_t)mp[0] >> (cbase & 7);
         else if constexpr (NC == 8) em[b] = mp[0];
@@ -413,7 +418,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
           const float d = ((em[b] >> j) & 1u) ? v[j] : 0.f;
           v[j] = d;
           s1[j] += d;
-          s2[j] += d * (xv - sh[j]);
+          s2[j] += be.x ? d * (xv - sh[j]) : 0.f;      // x == null: second partial 0
         }
 #pragma unroll
         for (int j = 0; j < NC / 2; ++j) pk[j] = cvt_pk_bf16(v[2 * j], v[2 * j + 1]);

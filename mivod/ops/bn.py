@@ -47,7 +47,7 @@ class GradSlot:
     (1 extra read).  Autograd still orders the producer after the tap: a None
     gradient satisfies the dependency edge.
     """
-    __slots__ = ("grad", "stride", "full_shape", "bn", "mode", "pending")
+    __slots__ = ("grad", "stride", "full_shape", "bn", "mode", "pending", "fold")
 
     def __init__(self):
         self.grad = None
@@ -60,6 +60,9 @@ class GradSlot:
         self.mode = 0
         # ... and its result (dz, partials), consumed by the BN backward
         self.pending = None
+        # producer is _Conv1x1BNFold: the consumer's reduce only needs sum dz (the
+        # producer derives sum dz (x - mean) from its weight-gradient GEMM)
+        self.fold = False
 
     def take(self):
         g, self.grad = self.grad, None
@@ -267,13 +270,18 @@ class BatchNorm2d(nn.BatchNorm2d):
         super().__init__(*a, **kw)
         self._mv_steps = 0   # host-side num_batches_tracked (saves a GPU add per call)
 
-    def forward(self, x, residual=None, relu=False, stats=None):
-        self._check_input_dim(x)
+    def _train_momentum(self) -> float:
+        """Momentum of this training forward (counts the step, as forward does)."""
         momentum = 0.0 if self.momentum is None else self.momentum
         if self.training and self.track_running_stats:
             self._mv_steps += 1
             if self.momentum is None:
                 momentum = 1.0 / float(self._mv_steps + int(self.num_batches_tracked.item()))
+        return momentum
+
+    def forward(self, x, residual=None, relu=False, stats=None):
+        self._check_input_dim(x)
+        momentum = self._train_momentum()
         bn_training = self.training or (self.running_mean is None and self.running_var is None)
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
@@ -395,6 +403,115 @@ def pad_channels(x: torch.Tensor, cout: int) -> torch.Tensor:
         else torch.contiguous_format)
 
 
+class _Conv1x1BNFold(torch.autograd.Function):
+    """``relu(bn(conv1x1(x)) + residual)`` (training, stride 1) with the BN backward folded
+    into the conv's backward GEMMs — the BN's input gradient dL/dz is never materialised.
+
+    With z = x W^T and the BN backward dL/dz = ca*dz + cb*z + cc (per output channel;
+    ca, cb, cc from the finalize of the reduce partials that the consuming conv's
+    data-gradient epilogue produced, ``slot.pending``; dz = the masked output gradient):
+        dx = dz (diag(ca) W) + x (W^T diag(cb) W) + cc W
+        dW = diag(ca) (dz^T x) + diag(cb) W (x^T x) + cc (x) colsum(x)
+    so the backward is two GEMMs for dx (hipBLASLt, bias = cc W), mivod's wgrad1x1 kernel
+    for dz^T x and the Gram matrix x^T x (fp32 out), and a few p x p / 4p x p products —
+    instead of the BN dx pass (read dz, z; write dL/dz) + dgrad + wgrad of dL/dz.  The
+    consumer's epilogue reduce only sums dz (``slot.fold``: z is not read there either);
+    sum dz (z - mean) = sum_k W[c, k] (dz^T x)[c, k] - mean * sum dz.  When no
+    consumer supplied the reduce (the stage's last blocks feeding a plain conv or the
+    pooling head) it runs the unfused BN backward and conv backward.
+    ``MIVOD_BN_FOLD=0`` disables it (A/B)."""
+
+    @staticmethod
+    def forward(ctx, x, w, weight, bias, running_mean, running_var, momentum, eps, residual,
+                slot, gemm):
+        nat = K.native()
+        n, cin, h, wd = x.shape
+        cout = w.shape[0]
+        if gemm:
+            m = n * h * wd
+            zf = torch.empty(m, cout, dtype=x.dtype, device=x.device)
+            part = torch.empty(nat.gemm_partials(m, cout, cin), 2, cout, dtype=torch.float32,
+                               device=x.device)
+            nat.gemm_nt(x.permute(0, 2, 3, 1).reshape(m, cin),
+                        w.permute(0, 2, 3, 1).reshape(cout, cin), zf, running_mean, part)
+            z = zf.view(n, h, wd, cout).permute(0, 3, 1, 2)
+            y, vec, keep = nat.bn_fwd_train_stats(z, part, weight, bias, running_mean, running_var,
+                                                  momentum, eps, True, residual, True)
+        else:
+            z = F.conv2d(x, w)
+            y, vec, keep = nat.bn_fwd_train_mask(z, weight, bias, running_mean, running_var,
+                                                 momentum, eps, residual)
+        ctx.save_for_backward(x, w, z, keep, vec, weight)
+        ctx.slot = slot
+        slot.bn = (z, keep, vec)
+        slot.mode = 3
+        slot.fold = True
+        ctx.set_materialize_grads(False)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .conv import _transposed_filter, wgrad1x1
+        x, w, z, keep, vec, weight = ctx.saved_tensors
+        slot = ctx.slot
+        slot.bn = None
+        pending, slot.pending = slot.pending, None
+        nat = K.native()
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        if pending is not None and dy is None:
+            dz, part = pending
+            assert slot.grad is None, "a tapped output has one shortcut consumer"
+            n, cin, h, wd = x.shape
+            cout, m = w.shape[0], n * h * wd
+            w2 = w.reshape(cout, cin).float()
+            x2 = x.permute(0, 2, 3, 1).reshape(m, cin)
+            g = nat.wgrad1x1(x, dz, 1, True).view(cout, cin)          # dz^T x
+            # the consumer's epilogue summed dz only: sum dz (z - mean) = rowdot(W, G) -
+            # mean * sum dz, with z = x W^T
+            sdz = part[:, 0].sum(0)
+            sdzx = (w2 * g).sum(1) - vec[0] * sdz
+            co = nat.bn_bwd_coeffs(vec, weight, torch.stack((sdz, sdzx)).unsqueeze(0), m)
+            dg, db, ca, cb, cc = co[0], co[1], co[2], co[3], co[4]
+            if need_w:
+                gram = nat.wgrad1x1(x, x, 1, True).view(cin, cin)
+                xs = nat.bn_stats(x, None, None, None, None, 0.0, 0.0)[0] * float(m)
+                dwf = torch.addcmul(ca[:, None] * g, cb[:, None], w2 @ gram)
+                dwf.addr_(cc, xs)
+                dw = dwf.to(w.dtype).view(cout, cin, 1, 1)
+            if need_x:
+                bp = (ca[:, None] * w2).to(x.dtype)
+                q = (w2.t() @ (cb[:, None] * w2)).to(x.dtype)
+                dx2 = torch.addmm((cc @ w2).to(x.dtype), dz.permute(0, 2, 3, 1).reshape(m, cout), bp)
+                dx2.addmm_(x2, q)
+                dx = dx2.view(n, h, wd, cin).permute(0, 3, 1, 2)
+        else:
+            if pending is not None:     # a further consumer: d = mask ? dy + dz : 0
+                dlz, dg, db, dz = nat.bn_bwd(3, _cl(dy), z, keep, vec, weight, True, pending[0], 1)
+            else:
+                dy = _cl(dy) if dy is not None else torch.zeros_like(z)
+                dy2, s2 = slot.take_strided()
+                dlz, dg, db, dz = nat.bn_bwd(3, dy, z, keep, vec, weight, True, dy2, s2)
+            if need_x:
+                dx = F.conv2d(dlz, _transposed_filter(w))
+            if need_w:
+                dw = wgrad1x1(dlz, x, w)
+        return (dx, dw, dg if ctx.needs_input_grad[2] else None,
+                db if ctx.needs_input_grad[3] else None, None, None, None, None,
+                dz if ctx.needs_input_grad[8] else None, None, None)
+
+
+def _fold_eligible(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu, residual) -> bool:
+    from .conv import _eligible
+    return (os.environ.get("MIVOD_BN_FOLD", "1") != "0" and relu and residual is not None
+            and _BN_MASK and bn.training and bn.track_running_stats
+            and bn.running_mean is not None and bn.weight is not None and bn.bias is not None
+            and _fusable(x, bn.weight) and residual.dtype == torch.bfloat16
+            and torch.is_grad_enabled() and x.requires_grad and _eligible(conv, x)
+            and tuple(conv.kernel_size) == (1, 1) and conv.in_channels % 64 == 0
+            and conv.out_channels % 64 == 0)
+
+
 def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = False,
             residual=None) -> torch.Tensor:
     """``bn(conv(x), residual, relu)`` with the BN statistics computed inside the
@@ -406,6 +523,15 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = Fa
                        stats_fusable)
     train_stats = (bn.training and bn.track_running_stats and bn.running_mean is not None
                    and _fusable(x, bn.weight))
+    if _fold_eligible(conv, bn, x, relu, residual):
+        residual = _cl(residual)
+        if residual.shape[0] == x.shape[0] and residual.shape[1] == conv.out_channels:
+            slot = GradSlot()
+            y = _Conv1x1BNFold.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean,
+                                     bn.running_var, float(bn._train_momentum()), float(bn.eps),
+                                     residual, slot, stats_fusable(conv, x))
+            y._mv_slot = slot
+            return y
     if conv3x3_eligible(conv, x):
         y, part = conv3x3_bn(conv, x, bn.running_mean if train_stats else None, train_stats,
                              bwd3x3_fusable(conv, x))

@@ -166,7 +166,8 @@ class _Conv1x1BN(torch.autograd.Function):
                 part = K.native().gemm_nt_bn_bwd(
                     dy.permute(0, 2, 3, 1).reshape(m, cout), w.reshape(cout, cin).t().contiguous(),
                     dz.permute(0, 2, 3, 1).reshape(m, cin), g2, mask,
-                    xb.permute(0, 2, 3, 1).reshape(m, cin), vec, 0, s2, h, wd)
+                    None if slot.fold else xb.permute(0, 2, 3, 1).reshape(m, cin), vec, 0, s2,
+                    h, wd)
                 slot.pending = (dz, part)
             else:
                 dx = F.conv2d(dy, _transposed_filter(w))

@@ -253,3 +253,64 @@ def test_resnet_bwd_fusion_matches_unfused(cuda, monkeypatch):
         ef = float((out["1"][k] - r).norm()) / n
         eu = float((out["0"][k] - r).norm()) / n
         assert ef <= 1.25 * eu + 2e-3, (k, ef, eu)
+
+
+def test_resnet_bn_fold_matches_unfolded(cuda, monkeypatch):
+    """ops.bn._Conv1x1BNFold: conv3 + BN3's backward as GEMMs on dz and x (BN dx never
+    materialised) — every parameter gradient as close to the fp32 eager reference as the
+    unfolded bf16 path's, and the folded branch really runs (bn_bwd_coeffs calls: the
+    blocks whose output feeds a fused conv1 data gradient)."""
+    import copy
+
+    from mivod.models.resnet import ResNet, to_mixed_bf16
+    nat = _nat()
+    calls = []
+    real = nat.bn_bwd_coeffs
+
+    def counted(*args, **kw):
+        calls.append(args[2].shape)
+        return real(*args, **kw)
+
+    monkeypatch.setattr(nat, "bn_bwd_coeffs", counted)
+    torch.manual_seed(0)
+    base = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
+    x = torch.rand(16, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    tgt = torch.randint(0, 10, (16,), device=cuda)
+
+    def grads(m, inp):
+        F.cross_entropy(m(inp).float(), tgt).backward()
+        return {k: p.grad.float() for k, p in m.named_parameters()}
+
+    ref = grads(copy.deepcopy(base).float(), x.float())
+    out = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("MIVOD_BN_FOLD", fold)
+        calls.clear()
+        out[fold] = grads(copy.deepcopy(base), x)
+        assert len(calls) == (5 if fold == "1" else 0), calls
+    for k, r in ref.items():
+        n = float(r.norm()) + 1e-12
+        ef = float((out["1"][k] - r).norm()) / n
+        eu = float((out["0"][k] - r).norm()) / n
+        assert ef <= 1.25 * eu + 2e-3, (k, ef, eu)
+
+
+def test_gemm_nt_bn_bwd_without_x(cuda):
+    """x = None: same dz and sum dz, second partial exactly 0 (the folded producer's path)."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(5)
+    M, K, N = 1000, 256, 64
+    a = torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).to(torch.bfloat16)
+    x = torch.randn(M, N, device=cuda, generator=g).to(torch.bfloat16)
+    vec = torch.randn(4, N, device=cuda, generator=g)
+    mask = torch.randint(0, 256, (M, N // 8), device=cuda, generator=g, dtype=torch.int32).to(
+        torch.uint8)
+    dz1, dz2 = torch.empty(M, N, device=cuda, dtype=torch.bfloat16), torch.empty(
+        M, N, device=cuda, dtype=torch.bfloat16)
+    p1 = nat.gemm_nt_bn_bwd(a, b, dz1, None, mask, x, vec)
+    p2 = nat.gemm_nt_bn_bwd(a, b, dz2, None, mask, None, vec)
+    assert torch.equal(dz1, dz2)
+    assert torch.equal(p1[:, 0], p2[:, 0])
+    assert not p2[:, 1].any()
