@@ -144,6 +144,9 @@ def test_resnet_uses_conv3x3_bwd_fusion(cuda, monkeypatch):
     monkeypatch.setattr(nat, "conv3x3_bn_bwd", counted)
     monkeypatch.setenv("MIVOD_CONV3X3_DGRAD", "1")     # every width (default: <= 128)
     monkeypatch.setenv("MIVOD_CONV1X1_BN_BWD", "1")    # opt-in (bench A/B neutral)
+    # the BN3 fold (ops.bn._Conv1x1BNFold) computes conv3's data gradient itself, so the
+    # 1x1 mode-1 reduce only runs with the fold off
+    monkeypatch.setenv("MIVOD_BN_FOLD", "0")
     torch.manual_seed(0)
     m = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
     x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
@@ -198,9 +201,10 @@ def test_resnet_uses_wgrad1x1(cuda, monkeypatch):
     calls = []
     real = nat.wgrad1x1
 
-    def counted(x, dy, s=1):
-        calls.append((x.shape[1], dy.shape[1], s))
-        return real(x, dy, s)
+    def counted(x, dy, s=1, *rest):
+        if not rest:        # the BN3 fold's fp32-output products (dz^T x, x^T x) aside
+            calls.append((x.shape[1], dy.shape[1], s))
+        return real(x, dy, s, *rest)
 
     monkeypatch.setattr(nat, "wgrad1x1", counted)
     torch.manual_seed(0)
