@@ -800,17 +800,29 @@ int64_t gemm_partials(int64_t M, int64_t N, int64_t K) {
   return mv_gemm_partials(M, (int)N, (int)K);
 }
 
-void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> shift,
-             c10::optional<at::Tensor> partial) {
-  for (const at::Tensor* t : {&a, &b, &c})
+void gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> co,
+             c10::optional<at::Tensor> shift, c10::optional<at::Tensor> partial) {
+  // c = None: statistics only (C is not written) — the recompute pass of ops.bn's fold
+  const bool has_c = co.has_value() && co->defined();
+  at::Tensor c = has_c ? *co : at::Tensor();
+  for (const at::Tensor* t : {&a, &b})
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
                     t->dim() == 2,
                 "gemm_nt: A, B, C must be contiguous 2-D bf16 GPU tensors");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_nt: shape mismatch");
+  if (has_c) {
+    TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kBFloat16 && c.is_contiguous() && c.dim() == 2,
+                "gemm_nt: C must be a contiguous 2-D bf16 GPU tensor");
+    TORCH_CHECK(c.size(0) == M && c.size(1) == N && a.device() == c.device(),
+                "gemm_nt: C shape/device mismatch");
+  } else {
+    TORCH_CHECK(partial.has_value() && mv_gemm_apply_supported((int)N, (int)K),
+                "gemm_nt: C may be omitted only for a statistics pass on a streamed shape");
+  }
+  TORCH_CHECK(b.size(1) == K, "gemm_nt: shape mismatch");
   TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && K > 0 && N > 0 && M > 0,
               "gemm_nt: K and N must be positive multiples of 64");
-  TORCH_CHECK(a.device() == b.device() && a.device() == c.device(), "gemm_nt: devices differ");
+  TORCH_CHECK(a.device() == b.device(), "gemm_nt: devices differ");
   TORCH_CHECK(M * K < (int64_t(1) << 40) && M * N < (int64_t(1) << 40), "gemm_nt: too large");
   TORCH_CHECK((M + 63) / 64 * (N / 64) < (int64_t(1) << 31), "gemm_nt: grid too large");
   float* pp = nullptr;
@@ -827,7 +839,60 @@ void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
     }
   }
   c10::DeviceGuard guard(a.device());
-  mv_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, (int)N, (int)K, sp, pp, cur_stream());
+  mv_gemm_nt(a.data_ptr(), b.data_ptr(), has_c ? c.data_ptr() : nullptr, M, (int)N, (int)K, sp,
+             pp, cur_stream());
+}
+
+bool gemm_apply_supported(int64_t N, int64_t K) { return mv_gemm_apply_supported((int)N, (int)K); }
+
+// {y, mask}: y = relu(bf16(a . b^T) * scale + bias + res) and its [M, N/8] bitmask (the
+// GEMM recomputed with the BN+add+ReLU apply in its epilogue)
+std::vector<at::Tensor> gemm_nt_apply(at::Tensor a, at::Tensor b, at::Tensor res, at::Tensor scale,
+                                      at::Tensor bias) {
+  for (const at::Tensor* t : {&a, &b, &res})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
+                    t->dim() == 2 && t->device() == a.device(),
+                "gemm_nt_apply: A, B, res must be contiguous 2-D bf16 tensors on one GPU");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(M > 0 && b.size(1) == K && res.size(0) == M && res.size(1) == N,
+              "gemm_nt_apply: shape mismatch");
+  TORCH_CHECK(mv_gemm_apply_supported((int)N, (int)K), "gemm_nt_apply: unsupported (K, N)");
+  TORCH_CHECK(M * K < (int64_t(1) << 40) && M * N < (int64_t(1) << 40), "gemm_nt_apply: too large");
+  for (const at::Tensor* t : {&scale, &bias})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                    t->numel() == N && t->device() == a.device(),
+                "gemm_nt_apply: scale/bias must be contiguous fp32 [N]");
+  c10::DeviceGuard guard(a.device());
+  at::Tensor y = at::empty({M, N}, res.options());
+  at::Tensor mask = at::empty({M, N / 8}, res.options().dtype(at::kByte));
+  TORCH_CHECK(mv_gemm_nt_apply(a.data_ptr(), b.data_ptr(), y.data_ptr(), M, (int)N, (int)K,
+                               res.data_ptr(), scale.data_ptr<float>(), bias.data_ptr<float>(),
+                               mask.data_ptr(), cur_stream()),
+              "gemm_nt_apply: launch failed");
+  return {y, mask};
+}
+
+// {4, C} saved statistics (mean, invstd, scale, bias) + running-stat update from [P, 2, C]
+// GEMM-epilogue partials of an M-row activation; no apply pass
+at::Tensor bn_finalize(at::Tensor stats, c10::optional<at::Tensor> gamma,
+                       c10::optional<at::Tensor> beta, c10::optional<at::Tensor> running_mean,
+                       c10::optional<at::Tensor> running_var, double momentum, double eps,
+                       int64_t M) {
+  TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kFloat && stats.is_contiguous() &&
+                  stats.dim() == 3 && stats.size(1) == 2 && stats.size(0) > 0 && M > 0,
+              "bn_finalize: stats must be fp32 [P, 2, C] partials");
+  const int64_t C = stats.size(2);
+  c10::DeviceGuard guard(stats.device());
+  at::Tensor vec = at::empty({4, C}, stats.options());
+  float* rm = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
+  float* rv = const_cast<float*>(opt_f32(running_var, C, "running_var"));
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "bn: running_mean/var must both be given");
+  mv_bn_fwd_from_partials(nullptr, nullptr, nullptr, M, (int)C, rm, rv, opt_f32(gamma, C, "weight"),
+                          opt_f32(beta, C, "bias"), (float)momentum, (float)eps, false,
+                          stats.data_ptr<float>(), (int)stats.size(0), vec[0].data_ptr<float>(),
+                          vec[1].data_ptr<float>(), vec[2].data_ptr<float>(),
+                          vec[3].data_ptr<float>(), cur_stream());
+  return vec;
 }
 
 int64_t gemm_bwd_partials(int64_t M, int64_t N, int64_t K, int64_t bn) {
@@ -1142,7 +1207,12 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gap_fwd", &gap_fwd, "NHWC global average pool -> [N, C]");
   m.def("gap_bwd", &gap_bwd, "NHWC global average pool backward");
   m.def("pad_channels", &pad_channels, "NHWC zero channel padding C -> cout (<= 8)");
-  m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics");
+  m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics "
+        "(C = None: statistics only)");
+  m.def("gemm_apply_supported", &gemm_apply_supported, "gemm_nt_apply handles (N, K)");
+  m.def("gemm_nt_apply", &gemm_nt_apply,
+        "{y, mask}: relu(bf16(A . B^T) * scale + bias + res) from the GEMM epilogue");
+  m.def("bn_finalize", &bn_finalize, "BN statistics finalize from [P, 2, C] partials -> [4, C]");
   m.def("gemm_nt_bn_bwd", &gemm_nt_bn_bwd,
         "1x1-conv data-gradient GEMM with the producing BN's add+ReLU backward reduce fused",
         py::arg("a"), py::arg("b"), py::arg("dz"), py::arg("dy2"), py::arg("mask"), py::arg("x"),

@@ -6,7 +6,8 @@
 // number of [2][N] statistics partial rows gemm_nt writes for this problem
 int64_t mv_gemm_partials(int64_t M, int N, int K);
 // C[M,N] = A[M,K] . B[N,K]^T (bf16 in/out, fp32 accumulate); K % 64 == 0, N % 64 == 0.
-// partial != null: fused BN statistics of C around shift -> partial[ceil(M/BM)][2][N]
+// partial != null: fused BN statistics of C around shift -> partial[ceil(M/BM)][2][N];
+// C == null (with partial): statistics only, C is not written (streamed shapes)
 void mv_gemm_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
                 const float* shift, float* partial, hipStream_t st);
 
@@ -22,3 +23,12 @@ bool mv_gemm_nt_bn_bwd(const void* A, const void* B, void* DZ, int64_t M, int N,
                        const void* dy2, const void* mask, const void* x, const float* mean,
                        float* partial, int bn, hipStream_t st, int dy2_stride = 1, int H = 1,
                        int W = 1);
+
+// BN(+residual)+ReLU apply fused into the GEMM epilogue (EPI 3 of the streaming kernel):
+// z = bf16(A . B^T), Y = relu(z * scale + bias + res) and the [M, N/8] bitmask of Y > 0 —
+// bit-identical to gemm_nt's z followed by mv_bn.hip's apply (ops.bn._Conv1x1BNFold's
+// recompute forward: statistics pass with C == null, finalize, then this)
+bool mv_gemm_apply_supported(int N, int K);
+bool mv_gemm_nt_apply(const void* A, const void* B, void* Y, int64_t M, int N, int K,
+                      const void* res, const float* scale, const float* bias, void* mask,
+                      hipStream_t st);

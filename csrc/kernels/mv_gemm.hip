@@ -235,6 +235,11 @@ struct BwdEpi {
   // of a strided 1x1 shortcut conv, ops/bn.py downsample_tap): row (n, h, w) adds
   // dy2[n, h/ds, w/ds] when h and w are multiples of ds
   int ds, H, W;
+  // EPI 3 (BN apply): y = relu(c * sc + bi + dy2) with dy2 = the residual, bitmask of y > 0
+  // -> mo ([M, N/8], mv_bn.hip's mode-3 layout)
+  const float* sc;
+  const float* bi;
+  uint8_t* mo;
 };
 
 // raw 16-/8-byte loads of NC consecutive bf16 (issued early, unpacked in the epilogue)
@@ -300,6 +305,15 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
     }
   };
   float sh[NC], s1[NC], s2[NC];
+  float apl_sc[EPI == 3 ? NC : 1], apl_bi[EPI == 3 ? NC : 1];
+  if constexpr (EPI == 3) {
+    static_assert(NC == 8 || NC == 16, "EPI 3 writes whole mask bytes");
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      apl_sc[j] = be.sc[cbase + j];
+      apl_bi[j] = be.bi[cbase + j];
+    }
+  }
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
     sh[j] = 0.f;
@@ -311,9 +325,17 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
   int64_t mt = stream;
   if (mt < ntm) gload(mt);
   for (; mt < ntm; mt += nstreams) {
-    // EPI 2: this tile's epilogue operands, in flight during the MFMA work
-    uint32_t e2[EPI == 2 ? TM : 1][NC / 2], ex[EPI == 2 ? TM : 1][NC / 2];
+    // EPI 2 / 3: this tile's epilogue operands, in flight during the MFMA work
+    uint32_t e2[EPI >= 2 ? TM : 1][NC / 2], ex[EPI == 2 ? TM : 1][NC / 2];
     uint32_t em[EPI == 2 ? TM : 1];
+    if constexpr (EPI == 3) {
+#pragma unroll
+      for (int b = 0; b < TM; ++b) {
+        int64_t row = mt * BM + b * 16 + rl;
+        row = row < M ? row : M - 1;
+        ld_raw<NC>(be.dy2 + row * N + cbase, e2[b]);
+      }
+    }
     if constexpr (EPI == 2) {
 #pragma unroll
       for (int b = 0; b < TM; ++b) {
@@ -423,6 +445,25 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
 #pragma unroll
         for (int j = 0; j < NC / 2; ++j) pk[j] = cvt_pk_bf16(v[2 * j], v[2 * j + 1]);
       }
+      if constexpr (EPI == 3) {
+        // mv_bn.hip apply_kernel's arithmetic on the bf16-rounded z: bit-identical y
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const float r = (j & 1) ? bf_hi(e2[b][j >> 1]) : bf_lo(e2[b][j >> 1]);
+          float a = __builtin_fmaf(v[j], apl_sc[j], apl_bi[j]);
+          a += r;
+          a = fmaxf(a, 0.f);
+          v[j] = a;
+          bits |= (a > 0.f ? 1u : 0u) << j;
+        }
+#pragma unroll
+        for (int j = 0; j < NC / 2; ++j) pk[j] = cvt_pk_bf16(v[2 * j], v[2 * j + 1]);
+        uint8_t* mp = be.mo + row * (N / 8) + cbase / 8;
+        if constexpr (NC == 8) *mp = (uint8_t)bits;
+        else *reinterpret_cast<uint16_t*>(mp) = (uint16_t)bits;
+      }
+      if (EPI == 1 && C == nullptr) continue;      // statistics only (the recompute pass)
       __bf16* cp = C + row * N + cbase;
       if constexpr (NC == 4) {
         *reinterpret_cast<u32x2*>(cp) = u32x2{pk[0], pk[1]};
@@ -434,7 +475,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       }
     }
   }
-  if (EPI == 0) return;
+  if (EPI == 0 || EPI == 3) return;
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
 #pragma unroll
@@ -541,6 +582,20 @@ static void launch_stream(const __bf16* a, const __bf16* b, __bf16* c, int64_t M
   }
 }
 
+// EPI 3 for the streamed (K, BN): BN >= 128, so a lane's NC channels fill whole mask bytes
+template <int K, int BN>
+static void launch_apply(const __bf16* a, const __bf16* b, __bf16* y, int64_t M, int N,
+                         const mv::gemm::BwdEpi& e, hipStream_t st) {
+  using namespace mv::gemm;
+  if constexpr (BN >= 128) {
+    const int ntn = N / BN;
+    const int64_t ntm = (M + 63) / 64;
+    const dim3 grid((unsigned)(streams_for<K, BN, 3>(M, N) * ntn));
+    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 3>), grid, dim3(256), 0, st, a, b, y, M, N, ntn,
+                       ntm, nullptr, nullptr, e);
+  }
+}
+
 #define MV_STREAM_CASES(X) \
   X(64, 256) X(64, 128) X(64, 64) X(128, 256) X(128, 128) X(128, 64) X(256, 128) X(256, 64)
 
@@ -619,5 +674,32 @@ bool mv_gemm_nt_bn_bwd(const void* A, const void* B, void* DZ, int64_t M, int N,
   if (K == KK && bn == BB) { launch_stream<KK, BB>(a, b, c, M, N, nullptr, partial, &e, st); return true; }
   MV_STREAM_CASES(MV_LB)
 #undef MV_LB
+  return false;
+}
+
+bool mv_gemm_apply_supported(int N, int K) {
+  int bn;
+  return K % 64 == 0 && N % 64 == 0 && stream_cfg(K, N, &bn) && bn >= 128;
+}
+
+bool mv_gemm_nt_apply(const void* A, const void* B, void* Y, int64_t M, int N, int K,
+                      const void* res, const float* scale, const float* bias, void* mask,
+                      hipStream_t st) {
+  using namespace mv::gemm;
+  int bn;
+  if (!mv_gemm_apply_supported(N, K) || !stream_cfg(K, N, &bn)) return false;
+  BwdEpi e{};
+  e.dy2 = (const __bf16*)res;
+  e.ds = 1;
+  e.sc = scale;
+  e.bi = bias;
+  e.mo = (uint8_t*)mask;
+  const __bf16* a = (const __bf16*)A;
+  const __bf16* b = (const __bf16*)B;
+  __bf16* y = (__bf16*)Y;
+#define MV_LA(KK, BB) \
+  if (K == KK && bn == BB && BB >= 128) { launch_apply<KK, BB>(a, b, y, M, N, e, st); return true; }
+  MV_STREAM_CASES(MV_LA)
+#undef MV_LA
   return false;
 }

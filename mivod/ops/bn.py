@@ -20,6 +20,8 @@ from . import kernels as K
 # MIVOD_BN_MASK=0: add+ReLU backward re-reads the bf16 output (mode 2) instead of the
 # forward's bitmask (mode 3) -- A/B switch
 _BN_MASK = os.environ.get("MIVOD_BN_MASK", "1") != "0"
+# MIVOD_BN_RECOMPUTE=0: the BN3 fold materialises z and runs the separate apply pass (A/B)
+_RECOMPUTE = os.environ.get("MIVOD_BN_RECOMPUTE", "1") != "0"
 
 
 def _fusable(x: torch.Tensor, weight) -> bool:
@@ -427,7 +429,24 @@ class _Conv1x1BNFold(torch.autograd.Function):
         nat = K.native()
         n, cin, h, wd = x.shape
         cout = w.shape[0]
-        if gemm:
+        if gemm and _RECOMPUTE and nat.gemm_apply_supported(cout, cin):
+            # z is never materialised: a statistics-only GEMM pass, the finalize, then the
+            # GEMM again with relu(bn(z) + residual) and the bitmask in its epilogue (the
+            # same tile order, so z and y are bit-identical to the two-pass path).  The
+            # expansion conv's z is the widest activation of the block: writing it and
+            # re-reading it in the apply pass costs more than a second K <= 256 GEMM.
+            m = n * h * wd
+            x2 = x.permute(0, 2, 3, 1).reshape(m, cin)
+            w2 = w.permute(0, 2, 3, 1).reshape(cout, cin)
+            part = torch.empty(nat.gemm_partials(m, cout, cin), 2, cout, dtype=torch.float32,
+                               device=x.device)
+            nat.gemm_nt(x2, w2, None, running_mean, part)
+            vec = nat.bn_finalize(part, weight, bias, running_mean, running_var, momentum, eps, m)
+            yf, keep = nat.gemm_nt_apply(x2, w2, residual.permute(0, 2, 3, 1).reshape(m, cout),
+                                         vec[2], vec[3])
+            y = yf.view(n, h, wd, cout).permute(0, 3, 1, 2)
+            z = None
+        elif gemm:
             m = n * h * wd
             zf = torch.empty(m, cout, dtype=x.dtype, device=x.device)
             part = torch.empty(nat.gemm_partials(m, cout, cin), 2, cout, dtype=torch.float32,
@@ -486,6 +505,13 @@ class _Conv1x1BNFold(torch.autograd.Function):
                 dx2.addmm_(x2, q)
                 dx = dx2.view(n, h, wd, cin).permute(0, 3, 1, 2)
         else:
+            if z is None:               # recompute forward: rebuild z (same GEMM, same bits)
+                n, cin, h, wd = x.shape
+                cout, m = w.shape[0], n * h * wd
+                zf = torch.empty(m, cout, dtype=x.dtype, device=x.device)
+                nat.gemm_nt(x.permute(0, 2, 3, 1).reshape(m, cin),
+                            w.permute(0, 2, 3, 1).reshape(cout, cin), zf, None, None)
+                z = zf.view(n, h, wd, cout).permute(0, 3, 1, 2)
             if pending is not None:     # a further consumer: d = mask ? dy + dz : 0
                 dlz, dg, db, dz = nat.bn_bwd(3, _cl(dy), z, keep, vec, weight, True, pending[0], 1)
             else:
