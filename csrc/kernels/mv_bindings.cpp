@@ -843,6 +843,41 @@ void gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> co,
              pp, cur_stream());
 }
 
+int64_t gemm_fold_dx_partials(int64_t M, int64_t K1, int64_t K2) {
+  return mv_gemm_fold_dx_partials(M, (int)K1, (int)K2);
+}
+
+// The BN3 fold's data gradient with BN2's ReLU backward reduce: d = relu'(bn2(xb)) *
+// ([a1 | a2] . b^T + badd) -> d (bf16 [M, K2]); returns the [P, 2, K2] partials
+at::Tensor gemm_fold_dx(at::Tensor a1, at::Tensor a2, at::Tensor b, at::Tensor badd, at::Tensor d,
+                        at::Tensor xb, at::Tensor vec) {
+  for (const at::Tensor* t : {&a1, &a2, &b, &d, &xb})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
+                    t->dim() == 2 && t->device() == a1.device(),
+                "gemm_fold_dx: A1, A2, B, D, xb must be contiguous 2-D bf16 tensors on one GPU");
+  const int64_t M = a1.size(0), K1 = a1.size(1), K2 = a2.size(1);
+  TORCH_CHECK(M > 0 && a2.size(0) == M && b.size(0) == K2 && b.size(1) == K1 + K2 &&
+                  d.size(0) == M && d.size(1) == K2 && xb.size(0) == M && xb.size(1) == K2,
+              "gemm_fold_dx: shape mismatch");
+  TORCH_CHECK(M * (K1 + K2) < (int64_t(1) << 40), "gemm_fold_dx: too large");
+  TORCH_CHECK(badd.is_cuda() && badd.scalar_type() == at::kFloat && badd.is_contiguous() &&
+                  badd.numel() == K2 && badd.device() == a1.device(),
+              "gemm_fold_dx: badd must be fp32 [K2]");
+  TORCH_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() &&
+                  vec.numel() == 4 * K2 && vec.device() == a1.device(),
+              "gemm_fold_dx: saved stats must be fp32 [4, K2]");
+  const int64_t P = mv_gemm_fold_dx_partials(M, (int)K1, (int)K2);
+  TORCH_CHECK(P > 0, "gemm_fold_dx: unsupported (K1, K2)");
+  c10::DeviceGuard guard(a1.device());
+  at::Tensor partial = at::empty({P, 2, K2}, a1.options().dtype(at::kFloat));
+  TORCH_CHECK(mv_gemm_fold_dx(a1.data_ptr(), a2.data_ptr(), b.data_ptr(), badd.data_ptr<float>(),
+                              d.data_ptr(), M, (int)K1, (int)K2, xb.data_ptr(),
+                              vec[0].data_ptr<float>(), vec[2].data_ptr<float>(),
+                              vec[3].data_ptr<float>(), partial.data_ptr<float>(), cur_stream()),
+              "gemm_fold_dx: launch failed");
+  return partial;
+}
+
 bool gemm_apply_supported(int64_t N, int64_t K) { return mv_gemm_apply_supported((int)N, (int)K); }
 
 // {y, mask}: y = relu(bf16(a . b^T) * scale + bias + res) and its [M, N/8] bitmask (the
@@ -1210,6 +1245,10 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics "
         "(C = None: statistics only)");
   m.def("gemm_apply_supported", &gemm_apply_supported, "gemm_nt_apply handles (N, K)");
+  m.def("gemm_fold_dx_partials", &gemm_fold_dx_partials,
+        "partial rows of gemm_fold_dx for (M, K1, K2) (-1: unsupported)");
+  m.def("gemm_fold_dx", &gemm_fold_dx,
+        "BN3-fold data gradient [a1|a2].b^T + badd with BN2's ReLU backward reduce -> partials");
   m.def("gemm_nt_apply", &gemm_nt_apply,
         "{y, mask}: relu(bf16(A . B^T) * scale + bias + res) from the GEMM epilogue");
   m.def("bn_finalize", &bn_finalize, "BN statistics finalize from [P, 2, C] partials -> [4, C]");

@@ -32,3 +32,12 @@ bool mv_gemm_apply_supported(int N, int K);
 bool mv_gemm_nt_apply(const void* A, const void* B, void* Y, int64_t M, int N, int K,
                       const void* res, const float* scale, const float* bias, void* mask,
                       hipStream_t st);
+
+// The BN3 fold's data gradient (ops.bn._Conv1x1BNFold) with the producing BN2's ReLU
+// backward reduce (EPI 4): dx = [A1 | A2] . B^T + badd (A1 = dz [M, K1], A2 = x [M, K2],
+// B = [K2, K1 + K2]), d = (fma(xb, scale, bias) > 0) ? bf16(dx) : 0 -> D [M, K2], partials
+// [P][2][K2] = (sum d, sum d (xb - mean)); (K1, K2) in {(256, 64), (512, 128)}.
+int64_t mv_gemm_fold_dx_partials(int64_t M, int K1, int K2);   // -1: unsupported
+bool mv_gemm_fold_dx(const void* A1, const void* A2, const void* B, const float* badd,
+                     void* D, int64_t M, int K1, int K2, const void* xb, const float* mean,
+                     const float* scale, const float* bias, float* partial, hipStream_t st);

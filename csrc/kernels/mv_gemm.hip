@@ -240,6 +240,11 @@ struct BwdEpi {
   const float* sc;
   const float* bi;
   uint8_t* mo;
+  // EPI 4 (the BN3 fold's data gradient with BN2's ReLU backward reduce): A's columns
+  // [K1, K) come from a2 ([M, K - K1]); badd [N] is added before rounding; the mask is
+  // fma(x, sc, bi) > 0 (x = the BN's input) and the partials are (sum d, sum d (x - mean))
+  const __bf16* a2;
+  const float* badd;
 };
 
 // raw 16-/8-byte loads of NC consecutive bf16 (issued early, unpacked in the epilogue)
@@ -262,7 +267,7 @@ __device__ __forceinline__ void ld_raw(const __bf16* p, uint32_t (&r)[NC / 2]) {
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-template <int K, int BN, int EPI, int BM = 64>
+template <int K, int BN, int EPI, int BM = 64, int K1 = K>
 __global__ __launch_bounds__(256) void gemm_stream_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
     int64_t M, int N, int ntn, int64_t ntm, const float* __restrict__ shift,
@@ -301,11 +306,25 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       const int q = tid + i * 256, row = q / KCH, ch = q % KCH;
       int64_t gm = m0 + row;
       gm = gm < M ? gm : M - 1;
-      ra[i] = *reinterpret_cast<const u32x4*>(A + gm * K + ch * 8);
+      if constexpr (K1 == K) {
+        ra[i] = *reinterpret_cast<const u32x4*>(A + gm * K + ch * 8);
+      } else {       // two row-major sources side by side along K
+        const __bf16* p = ch < K1 / 8 ? A + gm * K1 + ch * 8
+                                      : be.a2 + gm * (K - K1) + (ch - K1 / 8) * 8;
+        ra[i] = *reinterpret_cast<const u32x4*>(p);
+      }
     }
   };
   float sh[NC], s1[NC], s2[NC];
-  float apl_sc[EPI == 3 ? NC : 1], apl_bi[EPI == 3 ? NC : 1];
+  float apl_sc[EPI >= 3 ? NC : 1], apl_bi[EPI >= 3 ? NC : 1], add[EPI == 4 ? NC : 1];
+  if constexpr (EPI == 4) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      apl_sc[j] = be.sc[cbase + j];
+      apl_bi[j] = be.bi[cbase + j];
+      add[j] = be.badd[cbase + j];
+    }
+  }
   if constexpr (EPI == 3) {
     static_assert(NC == 8 || NC == 16, "EPI 3 writes whole mask bytes");
 #pragma unroll
@@ -318,7 +337,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
   for (int j = 0; j < NC; ++j) {
     sh[j] = 0.f;
     if (EPI == 1 && shift) sh[j] = shift[cbase + j];
-    if (EPI == 2) sh[j] = be.mean[cbase + j];
+    if (EPI == 2 || EPI == 4) sh[j] = be.mean[cbase + j];
     s1[j] = 0.f;
     s2[j] = 0.f;
   }
@@ -326,7 +345,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
   if (mt < ntm) gload(mt);
   for (; mt < ntm; mt += nstreams) {
     // EPI 2 / 3: this tile's epilogue operands, in flight during the MFMA work
-    uint32_t e2[EPI >= 2 ? TM : 1][NC / 2], ex[EPI == 2 ? TM : 1][NC / 2];
+    uint32_t e2[EPI == 2 || EPI == 3 ? TM : 1][NC / 2], ex[EPI == 2 || EPI == 4 ? TM : 1][NC / 2];
     uint32_t em[EPI == 2 ? TM : 1];
     if constexpr (EPI == 3) {
 #pragma unroll
@@ -334,6 +353,14 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
         int64_t row = mt * BM + b * 16 + rl;
         row = row < M ? row : M - 1;
         ld_raw<NC>(be.dy2 + row * N + cbase, e2[b]);
+      }
+    }
+    if constexpr (EPI == 4) {
+#pragma unroll
+      for (int b = 0; b < TM; ++b) {
+        int64_t row = mt * BM + b * 16 + rl;
+        row = row < M ? row : M - 1;
+        ld_raw<NC>(be.x + row * N + cbase, ex[b]);
       }
     }
     if constexpr (EPI == 2) {
@@ -409,6 +436,10 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       uint32_t pk[2 * TN];
 #pragma unroll
       for (int a = 0; a < TN; ++a) {
+        if constexpr (EPI == 4) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[a][b][r] += add[4 * a + r];
+        }
         pk[2 * a] = cvt_pk_bf16(acc[a][b][0], acc[a][b][1]);
         pk[2 * a + 1] = cvt_pk_bf16(acc[a][b][2], acc[a][b][3]);
       }
@@ -441,6 +472,19 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
           v[j] = d;
           s1[j] += d;
           s2[j] += be.x ? d * (xv - sh[j]) : 0.f;      // x == null: second partial 0
+        }
+#pragma unroll
+        for (int j = 0; j < NC / 2; ++j) pk[j] = cvt_pk_bf16(v[2 * j], v[2 * j + 1]);
+      }
+      if constexpr (EPI == 4) {
+        // mv_bn.hip bwd_reduce_kernel<1>: d = relu'(bn(x)) * dx on the bf16-rounded dx
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const float xv = (j & 1) ? bf_hi(ex[b][j >> 1]) : bf_lo(ex[b][j >> 1]);
+          const float d = __builtin_fmaf(xv, apl_sc[j], apl_bi[j]) > 0.f ? v[j] : 0.f;
+          v[j] = d;
+          s1[j] += d;
+          s2[j] += d * (xv - sh[j]);
         }
 #pragma unroll
         for (int j = 0; j < NC / 2; ++j) pk[j] = cvt_pk_bf16(v[2 * j], v[2 * j + 1]);
@@ -596,6 +640,31 @@ static void launch_apply(const __bf16* a, const __bf16* b, __bf16* y, int64_t M,
   }
 }
 
+// EPI 4 (dual-source A: K = K1 + K2, weight-stationary, 64-column tiles)
+template <int K, int K1>
+static bool launch_fold_dx(const __bf16* a, const __bf16* b, __bf16* d, int64_t M, int N,
+                           const mv::gemm::BwdEpi& e, float* partial, int64_t* P, hipStream_t st) {
+  using namespace mv::gemm;
+  constexpr int BN = 64;
+  static int per = [] {
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &v, (const void*)&gemm_stream_kernel<K, BN, 4, 64, K1>, 256, 0) != hipSuccess || v < 1)
+      v = 1;
+    return v;
+  }();
+  const int ntn = N / BN;
+  const int64_t ntm = (M + 63) / 64;
+  int64_t streams = (int64_t)num_cus() * per / ntn;
+  if (streams < 1) streams = 1;
+  if (streams > ntm) streams = ntm;
+  *P = streams;
+  if (!partial) return true;
+  hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 4, 64, K1>), dim3((unsigned)(streams * ntn)),
+                     dim3(256), 0, st, a, b, d, M, N, ntn, ntm, nullptr, partial, e);
+  return true;
+}
+
 #define MV_STREAM_CASES(X) \
   X(64, 256) X(64, 128) X(64, 64) X(128, 256) X(128, 128) X(128, 64) X(256, 128) X(256, 64)
 
@@ -702,4 +771,38 @@ bool mv_gemm_nt_apply(const void* A, const void* B, void* Y, int64_t M, int N, i
   MV_STREAM_CASES(MV_LA)
 #undef MV_LA
   return false;
+}
+
+// (K1, K2) = (cout, cin) of the folded conv: 256 + 64 (layer1), 512 + 128 (layer2)
+static bool fold_dx_dispatch(int K1, int K2, const __bf16* a, const __bf16* b, __bf16* d,
+                             int64_t M, int N, const mv::gemm::BwdEpi& e, float* partial,
+                             int64_t* P, hipStream_t st) {
+  if (N % 64 || N != K2) return false;
+  if (K1 == 256 && K2 == 64) return launch_fold_dx<320, 256>(a, b, d, M, N, e, partial, P, st);
+  if (K1 == 512 && K2 == 128) return launch_fold_dx<640, 512>(a, b, d, M, N, e, partial, P, st);
+  return false;
+}
+
+int64_t mv_gemm_fold_dx_partials(int64_t M, int K1, int K2) {
+  int64_t P = -1;
+  mv::gemm::BwdEpi e{};
+  if (!fold_dx_dispatch(K1, K2, nullptr, nullptr, nullptr, M, K2, e, nullptr, &P, nullptr))
+    return -1;
+  return P;
+}
+
+bool mv_gemm_fold_dx(const void* A1, const void* A2, const void* B, const float* badd,
+                     void* D, int64_t M, int K1, int K2, const void* x, const float* mean,
+                     const float* scale, const float* bias, float* partial, hipStream_t st) {
+  mv::gemm::BwdEpi e{};
+  e.x = (const __bf16*)x;
+  e.mean = mean;
+  e.sc = scale;
+  e.bi = bias;
+  e.a2 = (const __bf16*)A2;
+  e.badd = badd;
+  e.ds = 1;
+  int64_t P = 0;
+  return fold_dx_dispatch(K1, K2, (const __bf16*)A1, (const __bf16*)B, (__bf16*)D, M, K2, e,
+                          partial, &P, st);
 }

@@ -22,6 +22,9 @@ from . import kernels as K
 _BN_MASK = os.environ.get("MIVOD_BN_MASK", "1") != "0"
 # MIVOD_BN_RECOMPUTE=0: the BN3 fold materialises z and runs the separate apply pass (A/B)
 _RECOMPUTE = os.environ.get("MIVOD_BN_RECOMPUTE", "1") != "0"
+# MIVOD_BN_FOLD_DX=0: the fold's data gradient runs as two hipBLASLt GEMMs and BN2 runs its
+# own backward reduce pass, instead of mv_gemm's dual-source kernel with that reduce fused
+_FOLD_DX = os.environ.get("MIVOD_BN_FOLD_DX", "1") != "0"
 
 
 def _fusable(x: torch.Tensor, weight) -> bool:
@@ -414,9 +417,13 @@ class _Conv1x1BNFold(torch.autograd.Function):
     data-gradient epilogue produced, ``slot.pending``; dz = the masked output gradient):
         dx = dz (diag(ca) W) + x (W^T diag(cb) W) + cc W
         dW = diag(ca) (dz^T x) + diag(cb) W (x^T x) + cc (x) colsum(x)
-    so the backward is two GEMMs for dx (hipBLASLt, bias = cc W), mivod's wgrad1x1 kernel
-    for dz^T x and the Gram matrix x^T x (fp32 out), and a few p x p / 4p x p products —
-    instead of the BN dx pass (read dz, z; write dL/dz) + dgrad + wgrad of dL/dz.  The
+    so the backward is ONE dual-source GEMM for dx ([dz | x] . [diag(ca) W ; W^T diag(cb) W]
+    + cc W, mv_gemm's EPI 4, which also runs the ReLU backward reduce of BN2 — the producer
+    of x — in its epilogue; two hipBLASLt GEMMs on shapes it does not cover), mivod's
+    wgrad1x1 kernel for dz^T x and the Gram matrix x^T x (fp32 out), and a few p x p /
+    4p x p products — instead of the BN dx pass (read dz, z; write dL/dz) + dgrad + wgrad
+    of dL/dz.  Forward (``_RECOMPUTE``): z is never written — a statistics-only GEMM pass,
+    the finalize, then the GEMM again with the BN+add+ReLU apply in its epilogue.  The
     consumer's epilogue reduce only sums dz (``slot.fold``: z is not read there either);
     sum dz (z - mean) = sum_k W[c, k] (dz^T x)[c, k] - mean * sum dz.  When no
     consumer supplied the reduce (the stage's last blocks feeding a plain conv or the
@@ -462,6 +469,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
                                                  momentum, eps, residual)
         ctx.save_for_backward(x, w, z, keep, vec, weight)
         ctx.slot = slot
+        ctx.xslot = getattr(x, "_mv_slot", None)     # x = relu(bn2(z2)): BN2's GradSlot
         slot.bn = (z, keep, vec)
         slot.mode = 3
         slot.fold = True
@@ -498,7 +506,22 @@ class _Conv1x1BNFold(torch.autograd.Function):
                 dwf = torch.addcmul(ca[:, None] * g, cb[:, None], w2 @ gram)
                 dwf.addr_(cc, xs)
                 dw = dwf.to(w.dtype).view(cout, cin, 1, 1)
-            if need_x:
+            xs = ctx.xslot
+            if (need_x and _FOLD_DX and xs is not None and xs.bn is not None and xs.mode == 1
+                    and xs.pending is None and nat.gemm_fold_dx_partials(m, cout, cin) > 0):
+                # one dual-source GEMM [dz | x] . [diag(ca) W ; W^T diag(cb) W] + cc W with
+                # BN2's ReLU backward reduce in its epilogue: BN2 (the producer of x) gets
+                # (d, partials) through its slot and autograd gets None for x
+                zb, _, vec2 = xs.bn
+                bcat = torch.cat(((ca[:, None] * w2).t(), w2.t() @ (cb[:, None] * w2)), 1).to(
+                    x.dtype).contiguous()
+                d = torch.empty_like(zb)
+                part2 = nat.gemm_fold_dx(dz.permute(0, 2, 3, 1).reshape(m, cout), x2, bcat,
+                                         (cc @ w2).contiguous(),
+                                         d.permute(0, 2, 3, 1).reshape(m, cin),
+                                         zb.permute(0, 2, 3, 1).reshape(m, cin), vec2)
+                xs.pending = (d, part2)
+            elif need_x:
                 bp = (ca[:, None] * w2).to(x.dtype)
                 q = (w2.t() @ (cb[:, None] * w2)).to(x.dtype)
                 dx2 = torch.addmm((cc @ w2).to(x.dtype), dz.permute(0, 2, 3, 1).reshape(m, cout), bp)
