@@ -883,7 +883,8 @@ bool gemm_apply_supported(int64_t N, int64_t K) { return mv_gemm_apply_supported
 // {y, mask}: y = relu(bf16(a . b^T) * scale + bias + res) and its [M, N/8] bitmask (the
 // GEMM recomputed with the BN+add+ReLU apply in its epilogue)
 std::vector<at::Tensor> gemm_nt_apply(at::Tensor a, at::Tensor b, at::Tensor res, at::Tensor scale,
-                                      at::Tensor bias) {
+                                      at::Tensor bias, c10::optional<at::Tensor> rscale,
+                                      c10::optional<at::Tensor> rbias) {
   for (const at::Tensor* t : {&a, &b, &res})
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
                     t->dim() == 2 && t->device() == a.device(),
@@ -897,12 +898,22 @@ std::vector<at::Tensor> gemm_nt_apply(at::Tensor a, at::Tensor b, at::Tensor res
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
                     t->numel() == N && t->device() == a.device(),
                 "gemm_nt_apply: scale/bias must be contiguous fp32 [N]");
+  const bool raff = rscale.has_value() && rscale->defined();
+  TORCH_CHECK(raff == (rbias.has_value() && rbias->defined()),
+              "gemm_nt_apply: rscale and rbias go together");
+  if (raff)
+    for (const at::Tensor* t : {&*rscale, &*rbias})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                      t->numel() == N && t->device() == a.device(),
+                  "gemm_nt_apply: rscale/rbias must be contiguous fp32 [N]");
   c10::DeviceGuard guard(a.device());
   at::Tensor y = at::empty({M, N}, res.options());
   at::Tensor mask = at::empty({M, N / 8}, res.options().dtype(at::kByte));
   TORCH_CHECK(mv_gemm_nt_apply(a.data_ptr(), b.data_ptr(), y.data_ptr(), M, (int)N, (int)K,
                                res.data_ptr(), scale.data_ptr<float>(), bias.data_ptr<float>(),
-                               mask.data_ptr(), cur_stream()),
+                               mask.data_ptr(), cur_stream(),
+                               raff ? rscale->data_ptr<float>() : nullptr,
+                               raff ? rbias->data_ptr<float>() : nullptr),
               "gemm_nt_apply: launch failed");
   return {y, mask};
 }
@@ -1250,7 +1261,10 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_fold_dx", &gemm_fold_dx,
         "BN3-fold data gradient [a1|a2].b^T + badd with BN2's ReLU backward reduce -> partials");
   m.def("gemm_nt_apply", &gemm_nt_apply,
-        "{y, mask}: relu(bf16(A . B^T) * scale + bias + res) from the GEMM epilogue");
+        "{y, mask}: relu(bf16(A . B^T) * scale + bias + res) from the GEMM epilogue "
+        "(rscale/rbias: res = bf16(res * rscale + rbias), the shortcut BN's apply)",
+        py::arg("a"), py::arg("b"), py::arg("res"), py::arg("scale"), py::arg("bias"),
+        py::arg("rscale") = py::none(), py::arg("rbias") = py::none());
   m.def("bn_finalize", &bn_finalize, "BN statistics finalize from [P, 2, C] partials -> [4, C]");
   m.def("gemm_nt_bn_bwd", &gemm_nt_bn_bwd,
         "1x1-conv data-gradient GEMM with the producing BN's add+ReLU backward reduce fused",

@@ -29,9 +29,10 @@ bool mv_gemm_nt_bn_bwd(const void* A, const void* B, void* DZ, int64_t M, int N,
 // bit-identical to gemm_nt's z followed by mv_bn.hip's apply (ops.bn._Conv1x1BNFold's
 // recompute forward: statistics pass with C == null, finalize, then this)
 bool mv_gemm_apply_supported(int N, int K);
+// rscale != null: res is the shortcut BN's INPUT and bf16(res * rscale + rbias) is added
 bool mv_gemm_nt_apply(const void* A, const void* B, void* Y, int64_t M, int N, int K,
                       const void* res, const float* scale, const float* bias, void* mask,
-                      hipStream_t st);
+                      hipStream_t st, const float* rscale = nullptr, const float* rbias = nullptr);
 
 // The BN3 fold's data gradient (ops.bn._Conv1x1BNFold) with the producing BN2's ReLU
 // backward reduce (EPI 4): dx = [A1 | A2] . B^T + badd (A1 = dz [M, K1], A2 = x [M, K2],

@@ -245,6 +245,10 @@ struct BwdEpi {
   // fma(x, sc, bi) > 0 (x = the BN's input) and the partials are (sum d, sum d (x - mean))
   const __bf16* a2;
   const float* badd;
+  // EPI 5 = EPI 3 with an affine residual: the residual operand is the shortcut BN's input
+  // and bf16(fma(r, rsc, rbi)) is added (the shortcut BN's apply, bit-identical)
+  const float* rsc;
+  const float* rbi;
 };
 
 // raw 16-/8-byte loads of NC consecutive bf16 (issued early, unpacked in the epilogue)
@@ -316,7 +320,16 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
     }
   };
   float sh[NC], s1[NC], s2[NC];
+  constexpr bool APPLY = EPI == 3 || EPI == 5;
   float apl_sc[EPI >= 3 ? NC : 1], apl_bi[EPI >= 3 ? NC : 1], add[EPI == 4 ? NC : 1];
+  float res_sc[EPI == 5 ? NC : 1], res_bi[EPI == 5 ? NC : 1];
+  if constexpr (EPI == 5) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      res_sc[j] = be.rsc[cbase + j];
+      res_bi[j] = be.rbi[cbase + j];
+    }
+  }
   if constexpr (EPI == 4) {
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
@@ -325,7 +338,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       add[j] = be.badd[cbase + j];
     }
   }
-  if constexpr (EPI == 3) {
+  if constexpr (APPLY) {
     static_assert(NC == 8 || NC == 16, "EPI 3 writes whole mask bytes");
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
@@ -345,9 +358,9 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
   if (mt < ntm) gload(mt);
   for (; mt < ntm; mt += nstreams) {
     // EPI 2 / 3: this tile's epilogue operands, in flight during the MFMA work
-    uint32_t e2[EPI == 2 || EPI == 3 ? TM : 1][NC / 2], ex[EPI == 2 || EPI == 4 ? TM : 1][NC / 2];
+    uint32_t e2[EPI == 2 || APPLY ? TM : 1][NC / 2], ex[EPI == 2 || EPI == 4 ? TM : 1][NC / 2];
     uint32_t em[EPI == 2 ? TM : 1];
-    if constexpr (EPI == 3) {
+    if constexpr (APPLY) {
 #pragma unroll
       for (int b = 0; b < TM; ++b) {
         int64_t row = mt * BM + b * 16 + rl;
@@ -489,12 +502,13 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
 #pragma unroll
         for (int j = 0; j < NC / 2; ++j) pk[j] = cvt_pk_bf16(v[2 * j], v[2 * j + 1]);
       }
-      if constexpr (EPI == 3) {
+      if constexpr (APPLY) {
         // mv_bn.hip apply_kernel's arithmetic on the bf16-rounded z: bit-identical y
         uint32_t bits = 0;
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-          const float r = (j & 1) ? bf_hi(e2[b][j >> 1]) : bf_lo(e2[b][j >> 1]);
+          float r = (j & 1) ? bf_hi(e2[b][j >> 1]) : bf_lo(e2[b][j >> 1]);
+          if constexpr (EPI == 5) r = round_bf16(__builtin_fmaf(r, res_sc[j], res_bi[j]));
           float a = __builtin_fmaf(v[j], apl_sc[j], apl_bi[j]);
           a += r;
           a = fmaxf(a, 0.f);
@@ -519,7 +533,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       }
     }
   }
-  if (EPI == 0 || EPI == 3) return;
+  if (EPI == 0 || APPLY) return;
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
 #pragma unroll
@@ -634,9 +648,15 @@ static void launch_apply(const __bf16* a, const __bf16* b, __bf16* y, int64_t M,
   if constexpr (BN >= 128) {
     const int ntn = N / BN;
     const int64_t ntm = (M + 63) / 64;
-    const dim3 grid((unsigned)(streams_for<K, BN, 3>(M, N) * ntn));
-    hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 3>), grid, dim3(256), 0, st, a, b, y, M, N, ntn,
-                       ntm, nullptr, nullptr, e);
+    if (e.rsc) {
+      const dim3 grid((unsigned)(streams_for<K, BN, 5>(M, N) * ntn));
+      hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 5>), grid, dim3(256), 0, st, a, b, y, M, N,
+                         ntn, ntm, nullptr, nullptr, e);
+    } else {
+      const dim3 grid((unsigned)(streams_for<K, BN, 3>(M, N) * ntn));
+      hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 3>), grid, dim3(256), 0, st, a, b, y, M, N,
+                         ntn, ntm, nullptr, nullptr, e);
+    }
   }
 }
 
@@ -753,7 +773,7 @@ bool mv_gemm_apply_supported(int N, int K) {
 
 bool mv_gemm_nt_apply(const void* A, const void* B, void* Y, int64_t M, int N, int K,
                       const void* res, const float* scale, const float* bias, void* mask,
-                      hipStream_t st) {
+                      hipStream_t st, const float* rscale, const float* rbias) {
   using namespace mv::gemm;
   int bn;
   if (!mv_gemm_apply_supported(N, K) || !stream_cfg(K, N, &bn)) return false;
@@ -763,6 +783,8 @@ bool mv_gemm_nt_apply(const void* A, const void* B, void* Y, int64_t M, int N, i
   e.sc = scale;
   e.bi = bias;
   e.mo = (uint8_t*)mask;
+  e.rsc = rscale;
+  e.rbi = rscale ? rbias : nullptr;
   const __bf16* a = (const __bf16*)A;
   const __bf16* b = (const __bf16*)B;
   __bf16* y = (__bf16*)Y;

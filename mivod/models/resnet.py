@@ -16,9 +16,9 @@ import os
 
 import torch.nn.functional as F
 
-from ..ops.conv import Conv2d
+from ..ops.conv import Conv2d, conv1x1_stats, stats_fusable
 from ..ops.bn import (BatchNorm2d, bn_relu_maxpool, conv_bn, downsample_tap, global_avg_pool,
-                      pad_channels, tap)
+                      pad_channels, shortcut_fusable, tap)
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -79,6 +79,15 @@ class Bottleneck(nn.Module):
             identity = tap(x)
         else:
             conv, rest = self.downsample[0], self.downsample[1:]
+            if len(rest) == 1 and shortcut_fusable(self.conv3, self.bn3, out, rest[0]):
+                # the shortcut BN's apply runs inside conv3's recomputing GEMM epilogue: only
+                # the shortcut conv's output (and its BN statistics) is materialised
+                if conv.stride[0] == 1 and stats_fusable(conv, x):
+                    z, part = conv1x1_stats(conv, tap(x), rest[0].running_mean)
+                else:
+                    z, part = downsample_tap(x, conv), None
+                return conv_bn(self.conv3, self.bn3, out, relu=True, residual=z, res_bn=rest[0],
+                               res_part=part)
             if conv.stride[0] == 1 and len(rest) == 1 and isinstance(rest[0], BatchNorm2d):
                 identity = conv_bn(conv, rest[0], tap(x))
             else:

@@ -25,6 +25,9 @@ _RECOMPUTE = os.environ.get("MIVOD_BN_RECOMPUTE", "1") != "0"
 # MIVOD_BN_FOLD_DX=0: the fold's data gradient runs as two hipBLASLt GEMMs and BN2 runs its
 # own backward reduce pass, instead of mv_gemm's dual-source kernel with that reduce fused
 _FOLD_DX = os.environ.get("MIVOD_BN_FOLD_DX", "1") != "0"
+# MIVOD_BN_SHORTCUT=0: a projection shortcut's BN writes its output (identity) in its own
+# apply pass instead of being applied inside the recomputing conv3 GEMM's epilogue
+_SHORTCUT = os.environ.get("MIVOD_BN_SHORTCUT", "1") != "0"
 
 
 def _fusable(x: torch.Tensor, weight) -> bool:
@@ -432,10 +435,22 @@ class _Conv1x1BNFold(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, weight, bias, running_mean, running_var, momentum, eps, residual,
-                slot, gemm):
+                slot, gemm, res_w=None, res_b=None, res_cfg=None):
         nat = K.native()
         n, cin, h, wd = x.shape
         cout = w.shape[0]
+        vec_r = None
+        if res_cfg is not None:
+            # projection shortcut: residual is the shortcut BN's INPUT; its statistics come
+            # from the shortcut conv's GEMM epilogue (or a statistics pass) and its apply
+            # runs inside this GEMM's epilogue (conv_bn(..., res_bn=))
+            assert gemm and _RECOMPUTE and nat.gemm_apply_supported(cout, cin)
+            rm_r, rv_r, mom_r, eps_r, part_r = res_cfg
+            if part_r is not None:
+                vec_r = nat.bn_finalize(part_r, res_w, res_b, rm_r, rv_r, mom_r, eps_r,
+                                        n * h * wd)
+            else:
+                vec_r = nat.bn_stats(residual, res_w, res_b, rm_r, rv_r, mom_r, eps_r)
         if gemm and _RECOMPUTE and nat.gemm_apply_supported(cout, cin):
             # z is never materialised: a statistics-only GEMM pass, the finalize, then the
             # GEMM again with relu(bn(z) + residual) and the bitmask in its epilogue (the
@@ -450,7 +465,8 @@ class _Conv1x1BNFold(torch.autograd.Function):
             nat.gemm_nt(x2, w2, None, running_mean, part)
             vec = nat.bn_finalize(part, weight, bias, running_mean, running_var, momentum, eps, m)
             yf, keep = nat.gemm_nt_apply(x2, w2, residual.permute(0, 2, 3, 1).reshape(m, cout),
-                                         vec[2], vec[3])
+                                         vec[2], vec[3], None if vec_r is None else vec_r[2],
+                                         None if vec_r is None else vec_r[3])
             y = yf.view(n, h, wd, cout).permute(0, 3, 1, 2)
             z = None
         elif gemm:
@@ -467,7 +483,8 @@ class _Conv1x1BNFold(torch.autograd.Function):
             z = F.conv2d(x, w)
             y, vec, keep = nat.bn_fwd_train_mask(z, weight, bias, running_mean, running_var,
                                                  momentum, eps, residual)
-        ctx.save_for_backward(x, w, z, keep, vec, weight)
+        ctx.save_for_backward(x, w, z, keep, vec, weight, vec_r, res_w,
+                              residual if vec_r is not None else None)
         ctx.slot = slot
         ctx.xslot = getattr(x, "_mv_slot", None)     # x = relu(bn2(z2)): BN2's GradSlot
         slot.bn = (z, keep, vec)
@@ -479,7 +496,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         from .conv import _transposed_filter, wgrad1x1
-        x, w, z, keep, vec, weight = ctx.saved_tensors
+        x, w, z, keep, vec, weight, vec_r, res_w, zr = ctx.saved_tensors
         slot = ctx.slot
         slot.bn = None
         pending, slot.pending = slot.pending, None
@@ -545,9 +562,16 @@ class _Conv1x1BNFold(torch.autograd.Function):
                 dx = F.conv2d(dlz, _transposed_filter(w))
             if need_w:
                 dw = wgrad1x1(dlz, x, w)
+        dres = dz if ctx.needs_input_grad[8] else None
+        dgr = dbr = None
+        if vec_r is not None:
+            # the shortcut BN's backward (no activation) on the residual-branch gradient
+            dres, dgr, dbr, _ = nat.bn_bwd(0, _cl(dz), _cl(zr), None, vec_r, res_w, True, None, 1)
         return (dx, dw, dg if ctx.needs_input_grad[2] else None,
                 db if ctx.needs_input_grad[3] else None, None, None, None, None,
-                dz if ctx.needs_input_grad[8] else None, None, None)
+                dres if ctx.needs_input_grad[8] else None, None, None,
+                dgr if ctx.needs_input_grad[11] else None,
+                dbr if ctx.needs_input_grad[12] else None, None)
 
 
 def _fold_eligible(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu, residual) -> bool:
@@ -561,8 +585,21 @@ def _fold_eligible(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu, re
             and conv.out_channels % 64 == 0)
 
 
+def shortcut_fusable(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor,
+                     res_bn: nn.Module) -> bool:
+    """A projection shortcut's BN (``res_bn``) can be applied inside the epilogue of
+    conv3's recomputing GEMM (``conv_bn(conv, bn, x, True, z_shortcut, res_bn=...)``)."""
+    from .conv import stats_fusable
+    return (_SHORTCUT and _RECOMPUTE and isinstance(res_bn, BatchNorm2d) and res_bn.training
+            and res_bn.track_running_stats and res_bn.running_mean is not None
+            and res_bn.weight is not None and res_bn.bias is not None
+            and res_bn.weight.dtype == torch.float32
+            and _fold_eligible(conv, bn, x, True, x) and stats_fusable(conv, x)
+            and K.native().gemm_apply_supported(conv.out_channels, conv.in_channels))
+
+
 def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = False,
-            residual=None) -> torch.Tensor:
+            residual=None, res_bn=None, res_part=None) -> torch.Tensor:
     """``bn(conv(x), residual, relu)`` with the BN statistics computed inside the
     1x1 conv's GEMM epilogue when the conv qualifies (ops.conv.stats_fusable) and
     the BN is training with running statistics, and with x's producer BN backward
@@ -572,13 +609,28 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = Fa
                        stats_fusable)
     train_stats = (bn.training and bn.track_running_stats and bn.running_mean is not None
                    and _fusable(x, bn.weight))
+    if res_bn is not None:
+        # residual = the projection shortcut conv's output; res_bn = its BN (res_part: that
+        # BN's statistics partials from the shortcut GEMM's epilogue, or None)
+        residual = _cl(residual)
+        if (shortcut_fusable(conv, bn, x, res_bn) and residual.shape[0] == x.shape[0]
+                and residual.shape[1] == conv.out_channels):
+            slot = GradSlot()
+            cfg = (res_bn.running_mean, res_bn.running_var, float(res_bn._train_momentum()),
+                   float(res_bn.eps), res_part)
+            y = _Conv1x1BNFold.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean,
+                                     bn.running_var, float(bn._train_momentum()), float(bn.eps),
+                                     residual, slot, True, res_bn.weight, res_bn.bias, cfg)
+            y._mv_slot = slot
+            return y
+        residual = res_bn(residual, stats=res_part)
     if _fold_eligible(conv, bn, x, relu, residual):
         residual = _cl(residual)
         if residual.shape[0] == x.shape[0] and residual.shape[1] == conv.out_channels:
             slot = GradSlot()
             y = _Conv1x1BNFold.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean,
                                      bn.running_var, float(bn._train_momentum()), float(bn.eps),
-                                     residual, slot, stats_fusable(conv, x))
+                                     residual, slot, stats_fusable(conv, x), None, None, None)
             y._mv_slot = slot
             return y
     if conv3x3_eligible(conv, x):

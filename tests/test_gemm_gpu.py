@@ -353,6 +353,14 @@ def test_gemm_nt_apply_matches_two_pass(cuda, M, K, N):
     # and against fp32 math (to bf16 rounding)
     ref = torch.relu(z.float() * vec2[2] + vec2[3] + res.float())
     torch.testing.assert_close(y2.float(), ref, rtol=1e-2, atol=1e-2)
+    # affine residual (a projection shortcut's BN applied in the epilogue) == that BN's
+    # apply pass materialising the identity first
+    rsc = torch.rand(N, device=cuda, generator=g) + 0.5
+    rbi = torch.randn(N, device=cuda, generator=g) * 0.1
+    ident = nat.bn_apply(r4, rsc, rbi, False, None).permute(0, 2, 3, 1).reshape(M, N)
+    y3, mask3 = nat.gemm_nt_apply(a, b, ident, vec2[2], vec2[3])
+    y4, mask4 = nat.gemm_nt_apply(a, b, res, vec2[2], vec2[3], rsc, rbi)
+    assert torch.equal(y3, y4) and torch.equal(mask3, mask4)
 
 
 def test_gemm_nt_apply_rejects_unsupported(cuda):
@@ -478,3 +486,50 @@ def test_resnet_fold_dx_matches_hipblaslt(cuda, monkeypatch):
         e1 = float((out[True][k] - r).norm()) / n
         e0 = float((out[False][k] - r).norm()) / n
         assert e1 <= 1.25 * e0 + 2e-2, (k, e1, e0)
+
+
+def test_resnet_shortcut_bn_in_epilogue(cuda, monkeypatch):
+    """Projection-shortcut BNs applied inside conv3's recomputing GEMM (ops.bn._SHORTCUT):
+    the fused path runs for the stride-1 and strided shortcuts it covers, the running
+    statistics match the materialised path, and every parameter gradient is as close to
+    the fp32 reference as the materialised path's."""
+    import copy
+
+    from mivod.models.resnet import ResNet, to_mixed_bf16
+    from mivod.ops import bn as B
+    nat = _nat()
+    calls = []
+    real = nat.gemm_nt_apply
+
+    def counted(*args):
+        calls.append(len(args) > 5 and args[5] is not None)
+        return real(*args)
+
+    monkeypatch.setattr(nat, "gemm_nt_apply", counted)
+    torch.manual_seed(0)
+    base = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
+    x = torch.rand(16, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    tgt = torch.randint(0, 10, (16,), device=cuda)
+
+    def grads(m, inp):
+        F.cross_entropy(m(inp).float(), tgt).backward()
+        return ({k: p.grad.float() for k, p in m.named_parameters()},
+                {k: v.float() for k, v in m.state_dict().items() if "running" in k})
+
+    ref, _ = grads(copy.deepcopy(base).float(), x.float())
+    out, stats = {}, {}
+    for on in (True, False):
+        monkeypatch.setattr(B, "_SHORTCUT", on)
+        calls.clear()
+        out[on], stats[on] = grads(copy.deepcopy(base), x)
+        # layer1.0 (stride 1), layer2.0, layer3.0 (strided); layer4's conv3 (K 512) is not
+        # a recomputed GEMM
+        assert sum(calls) == (3 if on else 0), calls
+    for k, r in ref.items():
+        n = float(r.norm()) + 1e-12
+        e1 = float((out[True][k] - r).norm()) / n
+        e0 = float((out[False][k] - r).norm()) / n
+        assert e1 <= 1.25 * e0 + 2e-2, (k, e1, e0)
+    for k, r in stats[False].items():
+        torch.testing.assert_close(stats[True][k], r, rtol=1e-3, atol=1e-3)
