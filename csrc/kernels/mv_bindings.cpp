@@ -878,6 +878,28 @@ at::Tensor gemm_fold_dx(at::Tensor a1, at::Tensor a2, at::Tensor b, at::Tensor b
   return partial;
 }
 
+bool gemm_dual_supported(int64_t K1, int64_t K2) { return mv_gemm_dual_supported((int)K1, (int)K2); }
+
+// d = [a1 | a2] . b^T + badd (bf16 [M, K2])
+void gemm_dual_bias(at::Tensor a1, at::Tensor a2, at::Tensor b, at::Tensor badd, at::Tensor d) {
+  for (const at::Tensor* t : {&a1, &a2, &b, &d})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
+                    t->dim() == 2 && t->device() == a1.device(),
+                "gemm_dual_bias: A1, A2, B, D must be contiguous 2-D bf16 tensors on one GPU");
+  const int64_t M = a1.size(0), K1 = a1.size(1), K2 = a2.size(1);
+  TORCH_CHECK(M > 0 && a2.size(0) == M && b.size(0) == K2 && b.size(1) == K1 + K2 &&
+                  d.size(0) == M && d.size(1) == K2 && M * (K1 + K2) < (int64_t(1) << 40),
+              "gemm_dual_bias: shape mismatch");
+  TORCH_CHECK(badd.is_cuda() && badd.scalar_type() == at::kFloat && badd.is_contiguous() &&
+                  badd.numel() == K2 && badd.device() == a1.device(),
+              "gemm_dual_bias: badd must be fp32 [K2]");
+  TORCH_CHECK(mv_gemm_dual_supported((int)K1, (int)K2), "gemm_dual_bias: unsupported (K1, K2)");
+  c10::DeviceGuard guard(a1.device());
+  TORCH_CHECK(mv_gemm_dual_bias(a1.data_ptr(), a2.data_ptr(), b.data_ptr(), badd.data_ptr<float>(),
+                                d.data_ptr(), M, (int)K1, (int)K2, cur_stream()),
+              "gemm_dual_bias: launch failed");
+}
+
 bool gemm_apply_supported(int64_t N, int64_t K) { return mv_gemm_apply_supported((int)N, (int)K); }
 
 // {y, mask}: y = relu(bf16(a . b^T) * scale + bias + res) and its [M, N/8] bitmask (the
@@ -1256,6 +1278,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics "
         "(C = None: statistics only)");
   m.def("gemm_apply_supported", &gemm_apply_supported, "gemm_nt_apply handles (N, K)");
+  m.def("gemm_dual_supported", &gemm_dual_supported, "gemm_dual_bias handles (K1, K2)");
+  m.def("gemm_dual_bias", &gemm_dual_bias, "d = [a1 | a2] . b^T + badd (dual-source MFMA GEMM)");
   m.def("gemm_fold_dx_partials", &gemm_fold_dx_partials,
         "partial rows of gemm_fold_dx for (M, K1, K2) (-1: unsupported)");
   m.def("gemm_fold_dx", &gemm_fold_dx,

@@ -42,3 +42,9 @@ int64_t mv_gemm_fold_dx_partials(int64_t M, int K1, int K2);   // -1: unsupporte
 bool mv_gemm_fold_dx(const void* A1, const void* A2, const void* B, const float* badd,
                      void* D, int64_t M, int K1, int K2, const void* xb, const float* mean,
                      const float* scale, const float* bias, float* partial, hipStream_t st);
+
+// D[M, K2] = [A1 | A2] . B^T + badd (EPI 6: the dual-source GEMM of mv_gemm_fold_dx with a
+// plain store) — the projection-shortcut fold's input gradient; (K1, K2) = (256, 64) only
+bool mv_gemm_dual_supported(int K1, int K2);
+bool mv_gemm_dual_bias(const void* A1, const void* A2, const void* B, const float* badd, void* D,
+                       int64_t M, int K1, int K2, hipStream_t st);

@@ -321,7 +321,9 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
   };
   float sh[NC], s1[NC], s2[NC];
   constexpr bool APPLY = EPI == 3 || EPI == 5;
-  float apl_sc[EPI >= 3 ? NC : 1], apl_bi[EPI >= 3 ? NC : 1], add[EPI == 4 ? NC : 1];
+  // EPI 6: EPI 4's dual-source GEMM + badd with a plain store (no mask, no partials)
+  constexpr bool BADD = EPI == 4 || EPI == 6;
+  float apl_sc[EPI >= 3 ? NC : 1], apl_bi[EPI >= 3 ? NC : 1], add[BADD ? NC : 1];
   float res_sc[EPI == 5 ? NC : 1], res_bi[EPI == 5 ? NC : 1];
   if constexpr (EPI == 5) {
 #pragma unroll
@@ -335,8 +337,11 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
     for (int j = 0; j < NC; ++j) {
       apl_sc[j] = be.sc[cbase + j];
       apl_bi[j] = be.bi[cbase + j];
-      add[j] = be.badd[cbase + j];
     }
+  }
+  if constexpr (BADD) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) add[j] = be.badd[cbase + j];
   }
   if constexpr (APPLY) {
     static_assert(NC == 8 || NC == 16, "EPI 3 writes whole mask bytes");
@@ -449,7 +454,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       uint32_t pk[2 * TN];
 #pragma unroll
       for (int a = 0; a < TN; ++a) {
-        if constexpr (EPI == 4) {
+        if constexpr (BADD) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[a][b][r] += add[4 * a + r];
         }
@@ -533,7 +538,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       }
     }
   }
-  if (EPI == 0 || APPLY) return;
+  if (EPI == 0 || EPI == 6 || APPLY) return;
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
 #pragma unroll
@@ -661,7 +666,7 @@ static void launch_apply(const __bf16* a, const __bf16* b, __bf16* y, int64_t M,
 }
 
 // EPI 4 (dual-source A: K = K1 + K2, weight-stationary, 64-column tiles)
-template <int K, int K1>
+template <int K, int K1, int EPI = 4>
 static bool launch_fold_dx(const __bf16* a, const __bf16* b, __bf16* d, int64_t M, int N,
                            const mv::gemm::BwdEpi& e, float* partial, int64_t* P, hipStream_t st) {
   using namespace mv::gemm;
@@ -669,7 +674,7 @@ static bool launch_fold_dx(const __bf16* a, const __bf16* b, __bf16* d, int64_t 
   static int per = [] {
     int v = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &v, (const void*)&gemm_stream_kernel<K, BN, 4, 64, K1>, 256, 0) != hipSuccess || v < 1)
+            &v, (const void*)&gemm_stream_kernel<K, BN, EPI, 64, K1>, 256, 0) != hipSuccess || v < 1)
       v = 1;
     return v;
   }();
@@ -679,8 +684,8 @@ static bool launch_fold_dx(const __bf16* a, const __bf16* b, __bf16* d, int64_t 
   if (streams < 1) streams = 1;
   if (streams > ntm) streams = ntm;
   *P = streams;
-  if (!partial) return true;
-  hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 4, 64, K1>), dim3((unsigned)(streams * ntn)),
+  if (EPI == 4 ? !partial : !a) return true;
+  hipLaunchKernelGGL((gemm_stream_kernel<K, BN, EPI, 64, K1>), dim3((unsigned)(streams * ntn)),
                      dim3(256), 0, st, a, b, d, M, N, ntn, ntm, nullptr, partial, e);
   return true;
 }
@@ -827,4 +832,18 @@ bool mv_gemm_fold_dx(const void* A1, const void* A2, const void* B, const float*
   int64_t P = 0;
   return fold_dx_dispatch(K1, K2, (const __bf16*)A1, (const __bf16*)B, (__bf16*)D, M, K2, e,
                           partial, &P, st);
+}
+
+bool mv_gemm_dual_supported(int K1, int K2) { return K1 == 256 && K2 == 64; }
+
+bool mv_gemm_dual_bias(const void* A1, const void* A2, const void* B, const float* badd, void* D,
+                       int64_t M, int K1, int K2, hipStream_t st) {
+  if (!mv_gemm_dual_supported(K1, K2)) return false;
+  mv::gemm::BwdEpi e{};
+  e.a2 = (const __bf16*)A2;
+  e.badd = badd;
+  e.ds = 1;
+  int64_t P = 0;
+  return launch_fold_dx<320, 256, 6>((const __bf16*)A1, (const __bf16*)B, (__bf16*)D, M, K2, e,
+                                     nullptr, &P, st);
 }

@@ -18,7 +18,7 @@ import torch.nn.functional as F
 
 from ..ops.conv import Conv2d, conv1x1_stats, stats_fusable
 from ..ops.bn import (BatchNorm2d, bn_relu_maxpool, conv_bn, downsample_tap, global_avg_pool,
-                      pad_channels, shortcut_fusable, tap)
+                      pad_channels, shortcut_foldable, shortcut_fusable, tap)
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -81,7 +81,12 @@ class Bottleneck(nn.Module):
             conv, rest = self.downsample[0], self.downsample[1:]
             if len(rest) == 1 and shortcut_fusable(self.conv3, self.bn3, out, rest[0]):
                 # the shortcut BN's apply runs inside conv3's recomputing GEMM epilogue: only
-                # the shortcut conv's output (and its BN statistics) is materialised
+                # the shortcut conv's output (and its BN statistics) is materialised; with
+                # the shortcut fold the shortcut conv + BN backward also join the block's
+                # fused backward (x's gradient parked in its producer's slot)
+                if shortcut_foldable(conv, x):
+                    return conv_bn(self.conv3, self.bn3, out, relu=True, residual=x,
+                                   res_bn=rest[0], res_conv=conv)
                 if conv.stride[0] == 1 and stats_fusable(conv, x):
                     z, part = conv1x1_stats(conv, tap(x), rest[0].running_mean)
                 else:

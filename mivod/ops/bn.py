@@ -28,6 +28,10 @@ _FOLD_DX = os.environ.get("MIVOD_BN_FOLD_DX", "1") != "0"
 # MIVOD_BN_SHORTCUT=0: a projection shortcut's BN writes its output (identity) in its own
 # apply pass instead of being applied inside the recomputing conv3 GEMM's epilogue
 _SHORTCUT = os.environ.get("MIVOD_BN_SHORTCUT", "1") != "0"
+# MIVOD_BN_SHORTCUT_FOLD=0: the projection shortcut conv + BN keep their own backward (BN
+# reduce + dx passes, then the conv's data / weight gradients) instead of folding into
+# the block's fused backward
+_SHORTCUT_FOLD = os.environ.get("MIVOD_BN_SHORTCUT_FOLD", "1") != "0"
 
 
 def _fusable(x: torch.Tensor, weight) -> bool:
@@ -435,22 +439,46 @@ class _Conv1x1BNFold(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, weight, bias, running_mean, running_var, momentum, eps, residual,
-                slot, gemm, res_w=None, res_b=None, res_cfg=None):
+                slot, gemm, res_w=None, res_b=None, res_cfg=None, res_conv_w=None):
         nat = K.native()
         n, cin, h, wd = x.shape
         cout = w.shape[0]
         vec_r = None
+        sfold = res_conv_w is not None
+        ctx.sfold = sfold
         if res_cfg is not None:
-            # projection shortcut: residual is the shortcut BN's INPUT; its statistics come
-            # from the shortcut conv's GEMM epilogue (or a statistics pass) and its apply
-            # runs inside this GEMM's epilogue (conv_bn(..., res_bn=))
+            # projection shortcut: residual is the shortcut BN's INPUT (or, sfold, the
+            # shortcut CONV's input); its statistics come from the shortcut conv's GEMM
+            # epilogue (or a statistics pass) and its apply runs inside this GEMM's
+            # epilogue (conv_bn(..., res_bn=))
             assert gemm and _RECOMPUTE and nat.gemm_apply_supported(cout, cin)
-            rm_r, rv_r, mom_r, eps_r, part_r = res_cfg
+            rm_r, rv_r, mom_r, eps_r, part_r = res_cfg[:5]
+            if sfold:
+                s_r, ctx.x0slot = res_cfg[5], res_cfg[6]
+                ctx.s_r = s_r
+                c0 = residual.shape[1]
+                if s_r == 1 and c0 in (64, 128, 256):
+                    m0 = n * h * wd
+                    zrf = torch.empty(m0, cout, dtype=x.dtype, device=x.device)
+                    part_r = torch.empty(nat.gemm_partials(m0, cout, c0), 2, cout,
+                                         dtype=torch.float32, device=x.device)
+                    nat.gemm_nt(residual.permute(0, 2, 3, 1).reshape(m0, c0),
+                                res_conv_w.permute(0, 2, 3, 1).reshape(cout, c0), zrf, rm_r,
+                                part_r)
+                    zr_in = zrf.view(n, h, wd, cout).permute(0, 3, 1, 2)
+                else:
+                    zr_in = _cl(F.conv2d(residual, res_conv_w, None, s_r))
+                    part_r = None
+            else:
+                zr_in = residual
             if part_r is not None:
                 vec_r = nat.bn_finalize(part_r, res_w, res_b, rm_r, rv_r, mom_r, eps_r,
                                         n * h * wd)
             else:
-                vec_r = nat.bn_stats(residual, res_w, res_b, rm_r, rv_r, mom_r, eps_r)
+                vec_r = nat.bn_stats(zr_in, res_w, res_b, rm_r, rv_r, mom_r, eps_r)
+            residual_in = zr_in
+        else:
+            residual_in = residual
         if gemm and _RECOMPUTE and nat.gemm_apply_supported(cout, cin):
             # z is never materialised: a statistics-only GEMM pass, the finalize, then the
             # GEMM again with relu(bn(z) + residual) and the bitmask in its epilogue (the
@@ -464,7 +492,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
                                device=x.device)
             nat.gemm_nt(x2, w2, None, running_mean, part)
             vec = nat.bn_finalize(part, weight, bias, running_mean, running_var, momentum, eps, m)
-            yf, keep = nat.gemm_nt_apply(x2, w2, residual.permute(0, 2, 3, 1).reshape(m, cout),
+            yf, keep = nat.gemm_nt_apply(x2, w2, residual_in.permute(0, 2, 3, 1).reshape(m, cout),
                                          vec[2], vec[3], None if vec_r is None else vec_r[2],
                                          None if vec_r is None else vec_r[3])
             y = yf.view(n, h, wd, cout).permute(0, 3, 1, 2)
@@ -484,7 +512,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
             y, vec, keep = nat.bn_fwd_train_mask(z, weight, bias, running_mean, running_var,
                                                  momentum, eps, residual)
         ctx.save_for_backward(x, w, z, keep, vec, weight, vec_r, res_w,
-                              residual if vec_r is not None else None)
+                              residual if vec_r is not None else None, res_conv_w)
         ctx.slot = slot
         ctx.xslot = getattr(x, "_mv_slot", None)     # x = relu(bn2(z2)): BN2's GradSlot
         slot.bn = (z, keep, vec)
@@ -496,13 +524,14 @@ class _Conv1x1BNFold(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         from .conv import _transposed_filter, wgrad1x1
-        x, w, z, keep, vec, weight, vec_r, res_w, zr = ctx.saved_tensors
+        x, w, z, keep, vec, weight, vec_r, res_w, zr, res_conv_w = ctx.saved_tensors
         slot = ctx.slot
         slot.bn = None
         pending, slot.pending = slot.pending, None
         nat = K.native()
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dx = dw = None
+        sdz = None
         if pending is not None and dy is None:
             dz, part = pending
             assert slot.grad is None, "a tapped output has one shortcut consumer"
@@ -563,15 +592,59 @@ class _Conv1x1BNFold(torch.autograd.Function):
             if need_w:
                 dw = wgrad1x1(dlz, x, w)
         dres = dz if ctx.needs_input_grad[8] else None
-        dgr = dbr = None
-        if vec_r is not None:
+        dgr = dbr = dwr = None
+        if ctx.sfold:
+            # the shortcut conv + BN folded like conv3 + BN3 (zr = the conv's input x0):
+            # dz_sc = ca_r dz + cb_r (x0s W_r^T) + cc_r, so dx0 = [dz | x0s] . [diag(ca_r) W_r ;
+            # W_r^T diag(cb_r) W_r] + cc_r W_r and dW_r = diag(ca_r) dz^T x0s + diag(cb_r) W_r
+            # x0s^T x0s + cc_r colsum(x0s); the BN input z_sc is never read.  dx0 is parked in
+            # x0's producer slot (on the stride grid when s > 1), autograd gets None.
+            s_r = ctx.s_r
+            x0 = zr
+            nb, c0 = x0.shape[0], x0.shape[1]
+            cout_r = res_conv_w.shape[0]
+            x0s = x0 if s_r == 1 else _cl(x0[:, :, ::s_r, ::s_r])
+            ho, wo = x0s.shape[2], x0s.shape[3]
+            mr = nb * ho * wo
+            dzc = _cl(dz)
+            wr2 = res_conv_w.reshape(cout_r, c0).float()
+            gr = nat.wgrad1x1(x0, dzc, s_r, True).view(cout_r, c0)          # dz^T x0s
+            sdz_r = sdz if sdz is not None else torch.sum(dzc, (0, 2, 3), dtype=torch.float32)
+            sdzx_r = (wr2 * gr).sum(1) - vec_r[0] * sdz_r
+            co_r = nat.bn_bwd_coeffs(vec_r, res_w, torch.stack((sdz_r, sdzx_r)).unsqueeze(0), mr)
+            dgr, dbr, car, cbr, ccr = co_r[0], co_r[1], co_r[2], co_r[3], co_r[4]
+            if ctx.needs_input_grad[14]:
+                gram = nat.wgrad1x1(x0s, x0s, 1, True).view(c0, c0)
+                xsum = nat.bn_stats(x0s, None, None, None, None, 0.0, 0.0)[0] * float(mr)
+                dwf = torch.addcmul(car[:, None] * gr, cbr[:, None], wr2 @ gram)
+                dwf.addr_(ccr, xsum)
+                dwr = dwf.to(res_conv_w.dtype).view(cout_r, c0, 1, 1)
+            bcat = torch.cat(((car[:, None] * wr2).t(), wr2.t() @ (cbr[:, None] * wr2)), 1).to(
+                x0.dtype).contiguous()
+            badd = (ccr @ wr2).contiguous()
+            dz2d = dzc.permute(0, 2, 3, 1).reshape(mr, cout_r)
+            x02d = x0s.permute(0, 2, 3, 1).reshape(mr, c0)
+            if nat.gemm_dual_supported(cout_r, c0):
+                d0 = torch.empty(mr, c0, dtype=x0.dtype, device=x0.device)
+                nat.gemm_dual_bias(dz2d, x02d, bcat, badd, d0)
+            else:
+                d0 = torch.addmm(badd.to(x0.dtype), dz2d, bcat[:, :cout_r].t())
+                d0.addmm_(x02d, bcat[:, cout_r:].t())
+            d0 = d0.view(nb, ho, wo, c0).permute(0, 3, 1, 2)
+            s0 = ctx.x0slot
+            assert s0.grad is None, "a tapped output has one shortcut consumer"
+            s0.grad, s0.stride = d0, s_r
+            if s_r > 1:
+                s0.full_shape = x0.shape
+            dres = None
+        elif vec_r is not None:
             # the shortcut BN's backward (no activation) on the residual-branch gradient
             dres, dgr, dbr, _ = nat.bn_bwd(0, _cl(dz), _cl(zr), None, vec_r, res_w, True, None, 1)
         return (dx, dw, dg if ctx.needs_input_grad[2] else None,
                 db if ctx.needs_input_grad[3] else None, None, None, None, None,
                 dres if ctx.needs_input_grad[8] else None, None, None,
                 dgr if ctx.needs_input_grad[11] else None,
-                dbr if ctx.needs_input_grad[12] else None, None)
+                dbr if ctx.needs_input_grad[12] else None, None, dwr)
 
 
 def _fold_eligible(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu, residual) -> bool:
@@ -598,8 +671,20 @@ def shortcut_fusable(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor,
             and K.native().gemm_apply_supported(conv.out_channels, conv.in_channels))
 
 
+def shortcut_foldable(sc_conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """The projection shortcut conv ``sc_conv`` on the block input ``x`` can fold into the
+    block's fused backward (plain 1x1, x a fused output with a gradient slot)."""
+    return (_SHORTCUT_FOLD and getattr(x, "_mv_slot", None) is not None
+            and isinstance(sc_conv, nn.Conv2d) and tuple(sc_conv.kernel_size) == (1, 1)
+            and sc_conv.stride[0] == sc_conv.stride[1] and tuple(sc_conv.padding) == (0, 0)
+            and sc_conv.bias is None and sc_conv.groups == 1 and tuple(sc_conv.dilation) == (1, 1)
+            and sc_conv.weight.dtype == torch.bfloat16 and sc_conv.in_channels % 64 == 0
+            and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
+            and torch.is_grad_enabled() and x.requires_grad)
+
+
 def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = False,
-            residual=None, res_bn=None, res_part=None) -> torch.Tensor:
+            residual=None, res_bn=None, res_part=None, res_conv=None) -> torch.Tensor:
     """``bn(conv(x), residual, relu)`` with the BN statistics computed inside the
     1x1 conv's GEMM epilogue when the conv qualifies (ops.conv.stats_fusable) and
     the BN is training with running statistics, and with x's producer BN backward
@@ -612,6 +697,21 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = Fa
     if res_bn is not None:
         # residual = the projection shortcut conv's output; res_bn = its BN (res_part: that
         # BN's statistics partials from the shortcut GEMM's epilogue, or None)
+        # (res_conv: residual is that conv's INPUT, folded into this block's backward)
+        if res_conv is not None:
+            if shortcut_fusable(conv, bn, x, res_bn) and shortcut_foldable(res_conv, residual):
+                slot = GradSlot()
+                cfg = (res_bn.running_mean, res_bn.running_var, float(res_bn._train_momentum()),
+                       float(res_bn.eps), None, res_conv.stride[0], residual._mv_slot)
+                y = _Conv1x1BNFold.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean,
+                                         bn.running_var, float(bn._train_momentum()),
+                                         float(bn.eps), residual, slot, True, res_bn.weight,
+                                         res_bn.bias, cfg, res_conv.weight)
+                y._mv_slot = slot
+                return y
+            residual = res_bn(res_conv(tap(residual)))
+            res_bn = None
+    if res_bn is not None:
         residual = _cl(residual)
         if (shortcut_fusable(conv, bn, x, res_bn) and residual.shape[0] == x.shape[0]
                 and residual.shape[1] == conv.out_channels):
@@ -620,7 +720,7 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = Fa
                    float(res_bn.eps), res_part)
             y = _Conv1x1BNFold.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean,
                                      bn.running_var, float(bn._train_momentum()), float(bn.eps),
-                                     residual, slot, True, res_bn.weight, res_bn.bias, cfg)
+                                     residual, slot, True, res_bn.weight, res_bn.bias, cfg, None)
             y._mv_slot = slot
             return y
         residual = res_bn(residual, stats=res_part)
@@ -630,7 +730,8 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = Fa
             slot = GradSlot()
             y = _Conv1x1BNFold.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean,
                                      bn.running_var, float(bn._train_momentum()), float(bn.eps),
-                                     residual, slot, stats_fusable(conv, x), None, None, None)
+                                     residual, slot, stats_fusable(conv, x), None, None, None,
+                                     None)
             y._mv_slot = slot
             return y
     if conv3x3_eligible(conv, x):
