@@ -412,6 +412,21 @@ at::Tensor bn_apply(at::Tensor x, at::Tensor scale, at::Tensor bias, bool relu,
   return y;
 }
 
+// {y, partial}: y = relu(x * scale + bias) and [P, C] column-sum partials of y
+std::vector<at::Tensor> bn_apply_colsum(at::Tensor x, at::Tensor scale, at::Tensor bias) {
+  int64_t C;
+  const int64_t M = bn_check_act(x, "x", &C);
+  TORCH_CHECK(M > 0, "bn: empty input");
+  c10::DeviceGuard guard(x.device());
+  at::Tensor y = at::empty_like(x);
+  at::Tensor partial = at::empty({(int64_t)mv_bn_partials(M, (int)C), C},
+                                 x.options().dtype(at::kFloat));
+  const int P = mv_bn_apply_colsum(x.data_ptr(), y.data_ptr(), M, (int)C,
+                                   opt_f32(scale, C, "scale"), opt_f32(bias, C, "bias"),
+                                   partial.data_ptr<float>(), cur_stream());
+  return {y, partial.narrow(0, 0, P)};
+}
+
 // statistics only: running-stat update + saved {mean, invstd, scale, bias}; no apply pass
 at::Tensor bn_stats(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional<at::Tensor> beta,
                     c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
@@ -1270,6 +1285,8 @@ PYBIND11_MODULE(_mvk, m) {
         "fused BN(+add)(+ReLU) forward from the conv epilogue's statistics partials");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward (+ second grad stream)");
   m.def("bn_stats", &bn_stats, "NHWC BN training statistics only -> [4, C]");
+  m.def("bn_apply_colsum", &bn_apply_colsum,
+        "{y, [P, C] partials}: relu(x*scale + bias) with column sums of y");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC maxpool with fused affine+ReLU prologue -> (y, idx)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC maxpool backward (gather, + second grad stream)");
   m.def("gap_fwd", &gap_fwd, "NHWC global average pool -> [N, C]");

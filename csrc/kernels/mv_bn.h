@@ -39,3 +39,8 @@ void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const v
                int dy2_stride, int H, int W, hipStream_t st);
 // dy2_stride > 1: dy2 is [N, ceil(H/s), ceil(W/s), C] (gradient of a stride-s 1x1 conv's
 // input at its output resolution), added only on rows of the stride grid
+
+// y = relu(x * scale + bias) with [P][C] column-sum partials of the bf16 y (P returned,
+// <= mv_bn_partials(M, C))
+int mv_bn_apply_colsum(const void* x, void* y, int64_t M, int C, const float* scale,
+                       const float* bias, float* partial, hipStream_t st);

@@ -301,6 +301,66 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(const __bf16* __restrict_
   }
 }
 
+// BN + ReLU apply that also emits per-column sums of the bf16 OUTPUT (fixed-order
+// [P][C] partials): the colsum(x) term of a consumer 1x1 conv's folded BN backward
+// (ops.bn._Conv1x1BNFold: dW = ... + cc (x) colsum(x)) without a statistics pass over x.
+// No early return: every lane reaches the block reduction's barrier.
+template <int U>
+__global__ __launch_bounds__(kBlock) void apply_colsum_kernel(const __bf16* __restrict__ x,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ bias,
+                                                               __bf16* __restrict__ y, Geo g,
+                                                               float* __restrict__ partial) {
+  int tc, tr, c;
+  bool valid;
+  lane_map(g, &tc, &tr, &c, &valid);
+  float cs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs[j] = 0.f;
+  if (valid) {
+    float sc[8], bi[8];
+    load8f(scale + c, sc);
+    load8f(bias + c, bi);
+    const int64_t r0 = (int64_t)blockIdx.x * g.RB;
+    const int64_t r1 = (r0 + g.RB < g.M) ? r0 + g.RB : g.M;
+    int64_t r = r0 + tr;
+    for (; r + (U - 1) * g.RPI < r1; r += U * g.RPI) {
+      float v[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) ldlast<true>(x + (r + u * g.RPI) * g.C + c, v[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[u][j] = fmaxf(__builtin_fmaf(v[u][j], sc[j], bi[j]), 0.f);
+          cs[j] += (float)(__bf16)v[u][j];
+        }
+        store8(y + (r + u * g.RPI) * g.C + c, v[u]);
+      }
+    }
+    for (; r < r1; r += g.RPI) {
+      float v0[8];
+      ldlast<true>(x + r * g.C + c, v0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v0[j] = fmaxf(__builtin_fmaf(v0[j], sc[j], bi[j]), 0.f);
+        cs[j] += (float)(__bf16)v0[j];
+      }
+      store8(y + r * g.C + c, v0);
+    }
+  }
+  __shared__ float red[kBlock * kVec];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * kVec + j] = cs[j];
+  __syncthreads();
+  const int cb_eff = min(g.CB, g.C - (int)blockIdx.y * g.CB);
+  for (int cc = threadIdx.x; cc < cb_eff; cc += kBlock) {
+    float t = 0.f;
+    for (int q = 0; q < g.RPI; ++q) t += red[q * g.TPR * kVec + cc];
+    partial[(int64_t)blockIdx.x * g.C + blockIdx.y * g.CB + cc] = t;
+  }
+}
+
 // ---------------------------------------------------------------- backward
 // MODE 0: no activation (d = dy)
 // MODE 1: ReLU, mask recomputed from x:  d = (fma(x, scale, bias) > 0) ? dy : 0
@@ -760,4 +820,14 @@ void mv_bn_bwd_from_partials(const void* dz, const void* x, void* dx, int64_t M,
   if (dx)   // dx == nullptr: coefficients only (ops.conv._Conv1x1BNFold folds dx into its GEMMs)
     launch_bwd_dx<0>((const __bf16*)dz, (const __bf16*)x, scale, bias, ca, cb, cc, (__bf16*)dx, M,
                      C, st);
+}
+
+// y = relu(x * scale + bias) + [P][C] column-sum partials of y; returns P (<= mv_bn_partials)
+int mv_bn_apply_colsum(const void* x, void* y, int64_t M, int C, const float* scale,
+                       const float* bias, float* partial, hipStream_t st) {
+  Geo g = reduce_geo(M, C, mv_bn_partials(M, C), (const void*)&apply_colsum_kernel<2>);
+  const dim3 grid = grid_of(g);
+  hipLaunchKernelGGL(apply_colsum_kernel<2>, grid, dim3(kBlock), 0, st, (const __bf16*)x, scale,
+                     bias, (__bf16*)y, g, partial);
+  return (int)grid.x;
 }

@@ -68,7 +68,8 @@ class Bottleneck(nn.Module):
         # gradient also runs the backward reduce of the BN that produced x
         out = conv_bn(self.conv1, self.bn1, x, relu=True)
         # 3x3: mivod's implicit-GEMM conv with the BN statistics in its epilogue
-        out = conv_bn(self.conv2, self.bn2, out, relu=True)
+        # (+ column sums of the BN2 output for conv3's folded weight gradient)
+        out = conv_bn(self.conv2, self.bn2, out, relu=True, colsum=True)
         # the shortcut's gradient is added inside the backward of the op that
         # produced x (mivod.ops.bn.tap), not by a separate autograd add; a strided
         # 1x1 shortcut conv hands it over at its output resolution (downsample_tap).

@@ -32,6 +32,9 @@ _SHORTCUT = os.environ.get("MIVOD_BN_SHORTCUT", "1") != "0"
 # reduce + dx passes, then the conv's data / weight gradients) instead of folding into
 # the block's fused backward
 _SHORTCUT_FOLD = os.environ.get("MIVOD_BN_SHORTCUT_FOLD", "1") != "0"
+# MIVOD_BN_COLSUM=0: the fold's colsum(x) term reads x in a statistics pass instead of
+# taking BN2's apply-pass column sums
+_COLSUM = os.environ.get("MIVOD_BN_COLSUM", "1") != "0"
 
 
 def _fusable(x: torch.Tensor, weight) -> bool:
@@ -59,7 +62,7 @@ class GradSlot:
     (1 extra read).  Autograd still orders the producer after the tap: a None
     gradient satisfies the dependency edge.
     """
-    __slots__ = ("grad", "stride", "full_shape", "bn", "mode", "pending", "fold")
+    __slots__ = ("grad", "stride", "full_shape", "bn", "mode", "pending", "fold", "colsum")
 
     def __init__(self):
         self.grad = None
@@ -75,6 +78,9 @@ class GradSlot:
         # producer is _Conv1x1BNFold: the consumer's reduce only needs sum dz (the
         # producer derives sum dz (x - mean) from its weight-gradient GEMM)
         self.fold = False
+        # [P, C] column-sum partials of the output (BN+ReLU forward with colsum=True), for
+        # a folded consumer's dW term cc (x) colsum(x)
+        self.colsum = None
 
     def take(self):
         g, self.grad = self.grad, None
@@ -168,10 +174,15 @@ def tap(x: torch.Tensor) -> torch.Tensor:
 class _BNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, relu, residual,
-                slot, stats=None):
+                slot, stats=None, colsum=False):
         nat = K.native()
         mode = 2 if (relu and residual is not None) else (1 if relu else 0)
-        if stats is not None:
+        if stats is not None and mode == 1 and colsum and slot is not None:
+            vec = nat.bn_finalize(stats, weight, bias, running_mean, running_var, momentum, eps,
+                                  x.numel() // x.shape[1])
+            y, slot.colsum = nat.bn_apply_colsum(x, vec[2], vec[3])
+            keep = None
+        elif stats is not None:
             # statistics came from the producing 1x1 conv's GEMM epilogue (ops.conv)
             if mode == 2 and _BN_MASK:
                 y, vec, keep = nat.bn_fwd_train_stats(x, stats, weight, bias, running_mean,
@@ -226,7 +237,7 @@ class _BNActTrain(torch.autograd.Function):
                     dg if ctx.needs_input_grad[1] else None,
                     db if ctx.needs_input_grad[2] else None,
                     None, None, None, None, None, dz if ctx.needs_input_grad[8] else None,
-                    None, None)
+                    None, None, None)
         dy = _cl(dy) if dy is not None else torch.zeros_like(x)
         dy2, s2 = None, 1
         if ctx.slot is not None:
@@ -240,11 +251,11 @@ class _BNActTrain(torch.autograd.Function):
         return (dx if ctx.needs_input_grad[0] else None,
                 dg if ctx.needs_input_grad[1] else None,
                 db if ctx.needs_input_grad[2] else None,
-                None, None, None, None, None, dres, None, None)
+                None, None, None, None, None, dres, None, None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentum, eps,
-                   relu=False, residual=None, stats=None):
+                   relu=False, residual=None, stats=None, colsum=False):
     """Functional form: ``act(batch_norm(x) + residual)``.  ``stats``: [P, 2, C]
     statistics partials of x around ``running_mean`` from the producing conv's
     GEMM epilogue (training only; skips the statistics pass)."""
@@ -256,7 +267,7 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, training, momentu
             # mode 2/3: shortcut-gradient taps + fused consumer reduce; mode 1: fused reduce
             slot = GradSlot() if relu else None
             y = _BNActTrain.apply(x, weight, bias, running_mean, running_var, float(momentum),
-                                  float(eps), bool(relu), residual, slot, stats)
+                                  float(eps), bool(relu), residual, slot, stats, bool(colsum))
             if slot is not None:
                 y._mv_slot = slot
             return y
@@ -291,7 +302,7 @@ class BatchNorm2d(nn.BatchNorm2d):
                 momentum = 1.0 / float(self._mv_steps + int(self.num_batches_tracked.item()))
         return momentum
 
-    def forward(self, x, residual=None, relu=False, stats=None):
+    def forward(self, x, residual=None, relu=False, stats=None, colsum=False):
         self._check_input_dim(x)
         momentum = self._train_momentum()
         bn_training = self.training or (self.running_mean is None and self.running_var is None)
@@ -300,7 +311,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         if stats is not None and not (self.training and self.track_running_stats):
             stats = None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, bn_training, momentum, self.eps,
-                              relu, residual, stats)
+                              relu, residual, stats, colsum)
 
     def _save_to_state_dict(self, destination, prefix, keep_vars):
         if self._mv_steps and self.num_batches_tracked is not None:
@@ -515,6 +526,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
                               residual if vec_r is not None else None, res_conv_w)
         ctx.slot = slot
         ctx.xslot = getattr(x, "_mv_slot", None)     # x = relu(bn2(z2)): BN2's GradSlot
+        ctx.colsum = getattr(ctx.xslot, "colsum", None)
         slot.bn = (z, keep, vec)
         slot.mode = 3
         slot.fold = True
@@ -548,7 +560,10 @@ class _Conv1x1BNFold(torch.autograd.Function):
             dg, db, ca, cb, cc = co[0], co[1], co[2], co[3], co[4]
             if need_w:
                 gram = nat.wgrad1x1(x, x, 1, True).view(cin, cin)
-                xs = nat.bn_stats(x, None, None, None, None, 0.0, 0.0)[0] * float(m)
+                if ctx.colsum is not None:      # from BN2's apply pass
+                    xs = ctx.colsum.sum(0)
+                else:
+                    xs = nat.bn_stats(x, None, None, None, None, 0.0, 0.0)[0] * float(m)
                 dwf = torch.addcmul(ca[:, None] * g, cb[:, None], w2 @ gram)
                 dwf.addr_(cc, xs)
                 dw = dwf.to(w.dtype).view(cout, cin, 1, 1)
@@ -684,7 +699,8 @@ def shortcut_foldable(sc_conv: nn.Conv2d, x: torch.Tensor) -> bool:
 
 
 def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = False,
-            residual=None, res_bn=None, res_part=None, res_conv=None) -> torch.Tensor:
+            residual=None, res_bn=None, res_part=None, res_conv=None,
+            colsum: bool = False) -> torch.Tensor:
     """``bn(conv(x), residual, relu)`` with the BN statistics computed inside the
     1x1 conv's GEMM epilogue when the conv qualifies (ops.conv.stats_fusable) and
     the BN is training with running statistics, and with x's producer BN backward
@@ -737,7 +753,8 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu: bool = Fa
     if conv3x3_eligible(conv, x):
         y, part = conv3x3_bn(conv, x, bn.running_mean if train_stats else None, train_stats,
                              bwd3x3_fusable(conv, x))
-        return bn(y, residual=residual, relu=relu, stats=part if train_stats else None)
+        return bn(y, residual=residual, relu=relu, stats=part if train_stats else None,
+                  colsum=colsum and _COLSUM)
     fwd = train_stats and stats_fusable(conv, x)
     slot = bwd_fusable(conv, x)
     if fwd or slot is not None:

@@ -598,3 +598,60 @@ def test_resnet_shortcut_fold_matches_unfolded(cuda, monkeypatch):
         assert e1 <= 1.25 * e0 + 2e-2, (k, e1, e0)
     for k, r in stats[False].items():     # (MIOpen may pick another solution on a first call)
         torch.testing.assert_close(stats[True][k], r, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,C", [(1, 64), (3000, 64), (50000, 128), (777, 256), (4096, 512)])
+def test_bn_apply_colsum(cuda, M, C):
+    """BN+ReLU apply with column-sum partials == the plain apply (bitwise) + fp32 colsum."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(M + C)
+    x = torch.randn(M, C, device=cuda, generator=g).to(torch.bfloat16)
+    x4 = x.view(1, 1, M, C).permute(0, 3, 1, 2)
+    sc = torch.rand(C, device=cuda, generator=g) + 0.5
+    bi = torch.randn(C, device=cuda, generator=g) * 0.2
+    y1 = nat.bn_apply(x4, sc, bi, True, None)
+    y2, part = nat.bn_apply_colsum(x4, sc, bi)
+    assert torch.equal(y1, y2)
+    assert part.dim() == 2 and part.shape[1] == C and torch.isfinite(part).all()
+    ref = y1.permute(0, 2, 3, 1).reshape(M, C).float().sum(0)
+    torch.testing.assert_close(part.sum(0), ref, rtol=1e-4, atol=1e-2)
+
+
+def test_resnet_colsum_from_bn2_apply(cuda, monkeypatch):
+    """conv3's folded weight gradient takes colsum(x) from BN2's apply pass
+    (ops.bn._COLSUM) — same gradients (to fp32-reference closeness) and no statistics pass."""
+    import copy
+
+    from mivod.models.resnet import ResNet, to_mixed_bf16
+    from mivod.ops import bn as B
+    nat = _nat()
+    calls = []
+    real = nat.bn_apply_colsum
+
+    def counted(*args):
+        calls.append(args[0].shape)
+        return real(*args)
+
+    monkeypatch.setattr(nat, "bn_apply_colsum", counted)
+    torch.manual_seed(0)
+    base = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
+    x = torch.rand(16, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    tgt = torch.randint(0, 10, (16,), device=cuda)
+
+    def grads(m, inp):
+        F.cross_entropy(m(inp).float(), tgt).backward()
+        return {k: p.grad.float() for k, p in m.named_parameters()}
+
+    ref = grads(copy.deepcopy(base).float(), x.float())
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(B, "_COLSUM", on)
+        calls.clear()
+        out[on] = grads(copy.deepcopy(base), x)
+        assert (len(calls) > 0) == on, calls
+    for k, r in ref.items():
+        nr = float(r.norm()) + 1e-12
+        e1 = float((out[True][k] - r).norm()) / nr
+        e0 = float((out[False][k] - r).norm()) / nr
+        assert e1 <= 1.25 * e0 + 2e-2, (k, e1, e0)
