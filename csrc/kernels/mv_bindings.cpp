@@ -955,6 +955,38 @@ std::vector<at::Tensor> gemm_nt_apply(at::Tensor a, at::Tensor b, at::Tensor res
   return {y, mask};
 }
 
+bool gemm_apply_dual_supported(int64_t N, int64_t K) {
+  return mv_gemm_apply_dual_supported((int)N, (int)K);
+}
+
+// {y, mask}: relu(bf16(a . b^T) * scale + bias + bf16(bf16(a2 . b2^T) * rscale + rbias))
+std::vector<at::Tensor> gemm_nt_apply_dual(at::Tensor a, at::Tensor b, at::Tensor a2,
+                                           at::Tensor b2, at::Tensor scale, at::Tensor bias,
+                                           at::Tensor rscale, at::Tensor rbias) {
+  for (const at::Tensor* t : {&a, &b, &a2, &b2})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
+                    t->dim() == 2 && t->device() == a.device(),
+                "gemm_nt_apply_dual: A, B, A2, B2 must be contiguous 2-D bf16 tensors on one GPU");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(M > 0 && b.size(1) == K && a2.size(0) == M && a2.size(1) == K && b2.size(0) == N &&
+                  b2.size(1) == K && M * N < (int64_t(1) << 40),
+              "gemm_nt_apply_dual: shape mismatch");
+  TORCH_CHECK(mv_gemm_apply_dual_supported((int)N, (int)K), "gemm_nt_apply_dual: unsupported (K, N)");
+  for (const at::Tensor* t : {&scale, &bias, &rscale, &rbias})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                    t->numel() == N && t->device() == a.device(),
+                "gemm_nt_apply_dual: scale/bias/rscale/rbias must be contiguous fp32 [N]");
+  c10::DeviceGuard guard(a.device());
+  at::Tensor y = at::empty({M, N}, a.options());
+  at::Tensor mask = at::empty({M, N / 8}, a.options().dtype(at::kByte));
+  TORCH_CHECK(mv_gemm_nt_apply_dual(a.data_ptr(), b.data_ptr(), a2.data_ptr(), b2.data_ptr(),
+                                    y.data_ptr(), M, (int)N, (int)K, scale.data_ptr<float>(),
+                                    bias.data_ptr<float>(), rscale.data_ptr<float>(),
+                                    rbias.data_ptr<float>(), mask.data_ptr(), cur_stream()),
+              "gemm_nt_apply_dual: launch failed");
+  return {y, mask};
+}
+
 // {4, C} saved statistics (mean, invstd, scale, bias) + running-stat update from [P, 2, C]
 // GEMM-epilogue partials of an M-row activation; no apply pass
 at::Tensor bn_finalize(at::Tensor stats, c10::optional<at::Tensor> gamma,
@@ -1295,6 +1327,10 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics "
         "(C = None: statistics only)");
   m.def("gemm_apply_supported", &gemm_apply_supported, "gemm_nt_apply handles (N, K)");
+  m.def("gemm_apply_dual_supported", &gemm_apply_dual_supported,
+        "gemm_nt_apply_dual handles (N, K)");
+  m.def("gemm_nt_apply_dual", &gemm_nt_apply_dual,
+        "{y, mask}: the BN+add+ReLU apply GEMM with the shortcut conv + BN recomputed inside");
   m.def("gemm_dual_supported", &gemm_dual_supported, "gemm_dual_bias handles (K1, K2)");
   m.def("gemm_dual_bias", &gemm_dual_bias, "d = [a1 | a2] . b^T + badd (dual-source MFMA GEMM)");
   m.def("gemm_fold_dx_partials", &gemm_fold_dx_partials,

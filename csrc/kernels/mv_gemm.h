@@ -48,3 +48,11 @@ bool mv_gemm_fold_dx(const void* A1, const void* A2, const void* B, const float*
 bool mv_gemm_dual_supported(int K1, int K2);
 bool mv_gemm_dual_bias(const void* A1, const void* A2, const void* B, const float* badd, void* D,
                        int64_t M, int K1, int K2, hipStream_t st);
+
+// EPI 7: mv_gemm_nt_apply with the residual recomputed in the same kernel — y = relu(
+// bf16(A . B^T) * scale + bias + bf16(bf16(A2 . B2^T) * rscale + rbias)) (a stride-1
+// projection shortcut conv + BN on the block input A2 [M, K]; K == 64 only)
+bool mv_gemm_apply_dual_supported(int N, int K);
+bool mv_gemm_nt_apply_dual(const void* A, const void* B, const void* A2, const void* B2, void* Y,
+                           int64_t M, int N, int K, const float* scale, const float* bias,
+                           const float* rscale, const float* rbias, void* mask, hipStream_t st);

@@ -249,6 +249,9 @@ struct BwdEpi {
   // and bf16(fma(r, rsc, rbi)) is added (the shortcut BN's apply, bit-identical)
   const float* rsc;
   const float* rbi;
+  // EPI 7 = EPI 5 with the residual operand itself recomputed: r = bf16(a2 . b2^T) (the
+  // stride-1 projection shortcut conv; a2 [M, K], b2 [N, K]) — it is never written
+  const __bf16* b2;
 };
 
 // raw 16-/8-byte loads of NC consecutive bf16 (issued early, unpacked in the epilogue)
@@ -282,9 +285,12 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
   constexpr int WTN = BN / 4;                // columns per wave
   constexpr int TN = WTN / 16, TM = BM / 16;
   constexpr int NC = 4 * TN;                 // consecutive channels per lane
-  __shared__ __attribute__((aligned(16))) __bf16 smem[(BN + BM) * K];
+  constexpr bool DUAL = EPI == 7;             // second GEMM (a2 . b2^T) in the same tile loop
+  __shared__ __attribute__((aligned(16))) __bf16 smem[(BN + BM) * K * (DUAL ? 2 : 1)];
   __bf16* Ws = smem;
   __bf16* As = smem + BN * K;
+  __bf16* Ws2 = smem + (BN + BM) * K;        // DUAL only
+  __bf16* As2 = Ws2 + BN * K;
   auto sw = [](int row, int ch) { return row * K + ((ch ^ (row & 7)) << 3); };
 
   const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
@@ -301,8 +307,11 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
     const int q = tid + i * 256, row = q / KCH, ch = q % KCH;
     *reinterpret_cast<u32x4*>(Ws + sw(row, ch)) =
         *reinterpret_cast<const u32x4*>(B + (int64_t)(n0 + row) * K + ch * 8);
+    if constexpr (DUAL)
+      *reinterpret_cast<u32x4*>(Ws2 + sw(row, ch)) =
+          *reinterpret_cast<const u32x4*>(be.b2 + (int64_t)(n0 + row) * K + ch * 8);
   }
-  u32x4 ra[A_CH];
+  u32x4 ra[A_CH], ra2[DUAL ? A_CH : 1];
   auto gload = [&](int64_t mt) {
     const int64_t m0 = mt * BM;
 #pragma unroll
@@ -312,6 +321,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
       gm = gm < M ? gm : M - 1;
       if constexpr (K1 == K) {
         ra[i] = *reinterpret_cast<const u32x4*>(A + gm * K + ch * 8);
+        if constexpr (DUAL) ra2[i] = *reinterpret_cast<const u32x4*>(be.a2 + gm * K + ch * 8);
       } else {       // two row-major sources side by side along K
         const __bf16* p = ch < K1 / 8 ? A + gm * K1 + ch * 8
                                       : be.a2 + gm * (K - K1) + (ch - K1 / 8) * 8;
@@ -320,12 +330,13 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
     }
   };
   float sh[NC], s1[NC], s2[NC];
-  constexpr bool APPLY = EPI == 3 || EPI == 5;
+  constexpr bool APPLY = EPI == 3 || EPI == 5 || EPI == 7;
+  constexpr bool RAFF = EPI == 5 || EPI == 7;
   // EPI 6: EPI 4's dual-source GEMM + badd with a plain store (no mask, no partials)
   constexpr bool BADD = EPI == 4 || EPI == 6;
   float apl_sc[EPI >= 3 ? NC : 1], apl_bi[EPI >= 3 ? NC : 1], add[BADD ? NC : 1];
-  float res_sc[EPI == 5 ? NC : 1], res_bi[EPI == 5 ? NC : 1];
-  if constexpr (EPI == 5) {
+  float res_sc[RAFF ? NC : 1], res_bi[RAFF ? NC : 1];
+  if constexpr (RAFF) {
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
       res_sc[j] = be.rsc[cbase + j];
@@ -365,7 +376,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
     // EPI 2 / 3: this tile's epilogue operands, in flight during the MFMA work
     uint32_t e2[EPI == 2 || APPLY ? TM : 1][NC / 2], ex[EPI == 2 || EPI == 4 ? TM : 1][NC / 2];
     uint32_t em[EPI == 2 ? TM : 1];
-    if constexpr (APPLY) {
+    if constexpr (APPLY && !DUAL) {
 #pragma unroll
       for (int b = 0; b < TM; ++b) {
         int64_t row = mt * BM + b * 16 + rl;
@@ -422,6 +433,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
     for (int i = 0; i < A_CH; ++i) {
       const int q = tid + i * 256, row = q / KCH, ch = q % KCH;
       *reinterpret_cast<u32x4*>(As + sw(row, ch)) = ra[i];
+      if constexpr (DUAL) *reinterpret_cast<u32x4*>(As2 + sw(row, ch)) = ra2[i];
     }
     __syncthreads();
     if (mt + nstreams < ntm) gload(mt + nstreams);     // in flight during compute + stores
@@ -430,6 +442,38 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
     for (int a = 0; a < TN; ++a)
 #pragma unroll
       for (int b = 0; b < TM; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    if constexpr (DUAL) {
+      // the shortcut GEMM first: its bf16-rounded result becomes this tile's residual
+      // operand (packed like a prefetched residual row), then the main GEMM
+      f32x4v acc2[TN][TM];
+#pragma unroll
+      for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc2[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < K / 32; ++kk) {
+        const int ch = kk * 4 + g;
+        bf16x8 wf[TN], af[TM];
+#pragma unroll
+        for (int a = 0; a < TN; ++a)
+          wf[a] = *reinterpret_cast<const bf16x8*>(
+              Ws2 + sw(wn * WTN + NC * (rl >> 2) + 4 * a + (rl & 3), ch));
+#pragma unroll
+        for (int b = 0; b < TM; ++b)
+          af[b] = *reinterpret_cast<const bf16x8*>(As2 + sw(b * 16 + rl, ch));
+#pragma unroll
+        for (int a = 0; a < TN; ++a)
+#pragma unroll
+          for (int b = 0; b < TM; ++b) acc2[a][b] = mfma(wf[a], af[b], acc2[a][b]);
+      }
+#pragma unroll
+      for (int b = 0; b < TM; ++b)
+#pragma unroll
+        for (int a = 0; a < TN; ++a) {
+          e2[b][2 * a] = cvt_pk_bf16(acc2[a][b][0], acc2[a][b][1]);
+          e2[b][2 * a + 1] = cvt_pk_bf16(acc2[a][b][2], acc2[a][b][3]);
+        }
+    }
 #pragma unroll
     for (int kk = 0; kk < K / 32; ++kk) {
       const int ch = kk * 4 + g;
@@ -513,7 +557,7 @@ __global__ __launch_bounds__(256) void gemm_stream_kernel(
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
           float r = (j & 1) ? bf_hi(e2[b][j >> 1]) : bf_lo(e2[b][j >> 1]);
-          if constexpr (EPI == 5) r = round_bf16(__builtin_fmaf(r, res_sc[j], res_bi[j]));
+          if constexpr (RAFF) r = round_bf16(__builtin_fmaf(r, res_sc[j], res_bi[j]));
           float a = __builtin_fmaf(v[j], apl_sc[j], apl_bi[j]);
           a += r;
           a = fmaxf(a, 0.f);
@@ -653,7 +697,13 @@ static void launch_apply(const __bf16* a, const __bf16* b, __bf16* y, int64_t M,
   if constexpr (BN >= 128) {
     const int ntn = N / BN;
     const int64_t ntm = (M + 63) / 64;
-    if (e.rsc) {
+    if (e.b2) {
+      if constexpr (K == 64) {       // the stride-1 shortcut's K equals conv3's (layer1)
+        const dim3 grid((unsigned)(streams_for<K, BN, 7>(M, N) * ntn));
+        hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 7>), grid, dim3(256), 0, st, a, b, y, M, N,
+                           ntn, ntm, nullptr, nullptr, e);
+      }
+    } else if (e.rsc) {
       const dim3 grid((unsigned)(streams_for<K, BN, 5>(M, N) * ntn));
       hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 5>), grid, dim3(256), 0, st, a, b, y, M, N,
                          ntn, ntm, nullptr, nullptr, e);
@@ -846,4 +896,39 @@ bool mv_gemm_dual_bias(const void* A1, const void* A2, const void* B, const floa
   int64_t P = 0;
   return launch_fold_dx<320, 256, 6>((const __bf16*)A1, (const __bf16*)B, (__bf16*)D, M, K2, e,
                                      nullptr, &P, st);
+}
+
+bool mv_gemm_apply_dual_supported(int N, int K) {
+  int bn;
+  return K == 64 && mv_gemm_apply_supported(N, K) && stream_cfg(K, N, &bn) && bn >= 128;
+}
+
+bool mv_gemm_nt_apply_dual(const void* A, const void* B, const void* A2, const void* B2, void* Y,
+                           int64_t M, int N, int K, const float* scale, const float* bias,
+                           const float* rscale, const float* rbias, void* mask, hipStream_t st) {
+  if (!mv_gemm_apply_dual_supported(N, K) || !rscale || !rbias) return false;
+  using namespace mv::gemm;
+  int bn;
+  stream_cfg(K, N, &bn);
+  BwdEpi e{};
+  e.ds = 1;
+  e.sc = scale;
+  e.bi = bias;
+  e.mo = (uint8_t*)mask;
+  e.rsc = rscale;
+  e.rbi = rbias;
+  e.a2 = (const __bf16*)A2;
+  e.b2 = (const __bf16*)B2;
+  const __bf16* a = (const __bf16*)A;
+  const __bf16* b = (const __bf16*)B;
+  __bf16* y = (__bf16*)Y;
+  // 128-column tiles: the 256-wide tile's two accumulator sets leave 1 wave per SIMD
+  // (200 VGPRs + 116 AGPRs), the 128-wide one keeps 2 (MIVOD_GEMM_DUAL_BN=256 for A/B)
+  static const int want = [] {
+    const char* v = std::getenv("MIVOD_GEMM_DUAL_BN");
+    return v && std::atoi(v) == 256 ? 256 : 128;
+  }();
+  if (bn == 256 && want == 256) { launch_apply<64, 256>(a, b, y, M, N, e, st); return true; }
+  launch_apply<64, 128>(a, b, y, M, N, e, st);
+  return true;
 }

@@ -35,6 +35,9 @@ _SHORTCUT_FOLD = os.environ.get("MIVOD_BN_SHORTCUT_FOLD", "1") != "0"
 # MIVOD_BN_COLSUM=0: the fold's colsum(x) term reads x in a statistics pass instead of
 # taking BN2's apply-pass column sums
 _COLSUM = os.environ.get("MIVOD_BN_COLSUM", "1") != "0"
+# MIVOD_BN_SHORTCUT_DUAL=0: a stride-1 shortcut conv's output is written by its statistics
+# GEMM and read back as the residual, instead of being recomputed inside conv3's apply GEMM
+_SHORTCUT_DUAL = os.environ.get("MIVOD_BN_SHORTCUT_DUAL", "1") != "0"
 
 
 def _fusable(x: torch.Tensor, weight) -> bool:
@@ -468,7 +471,19 @@ class _Conv1x1BNFold(torch.autograd.Function):
                 s_r, ctx.x0slot = res_cfg[5], res_cfg[6]
                 ctx.s_r = s_r
                 c0 = residual.shape[1]
-                if s_r == 1 and c0 in (64, 128, 256):
+                dual = None
+                if (s_r == 1 and _SHORTCUT_DUAL and c0 == cin
+                        and nat.gemm_apply_dual_supported(cout, cin)):
+                    # z_sc is never written: statistics-only pass here, recomputed in the
+                    # apply GEMM below (EPI 7)
+                    m0 = n * h * wd
+                    dual = (residual.permute(0, 2, 3, 1).reshape(m0, c0),
+                            res_conv_w.permute(0, 2, 3, 1).reshape(cout, c0))
+                    part_r = torch.empty(nat.gemm_partials(m0, cout, c0), 2, cout,
+                                         dtype=torch.float32, device=x.device)
+                    nat.gemm_nt(dual[0], dual[1], None, rm_r, part_r)
+                    zr_in = None
+                elif s_r == 1 and c0 in (64, 128, 256):
                     m0 = n * h * wd
                     zrf = torch.empty(m0, cout, dtype=x.dtype, device=x.device)
                     part_r = torch.empty(nat.gemm_partials(m0, cout, c0), 2, cout,
@@ -481,7 +496,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
                     zr_in = _cl(F.conv2d(residual, res_conv_w, None, s_r))
                     part_r = None
             else:
-                zr_in = residual
+                zr_in, dual = residual, None
             if part_r is not None:
                 vec_r = nat.bn_finalize(part_r, res_w, res_b, rm_r, rv_r, mom_r, eps_r,
                                         n * h * wd)
@@ -489,7 +504,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
                 vec_r = nat.bn_stats(zr_in, res_w, res_b, rm_r, rv_r, mom_r, eps_r)
             residual_in = zr_in
         else:
-            residual_in = residual
+            residual_in, dual = residual, None
         if gemm and _RECOMPUTE and nat.gemm_apply_supported(cout, cin):
             # z is never materialised: a statistics-only GEMM pass, the finalize, then the
             # GEMM again with relu(bn(z) + residual) and the bitmask in its epilogue (the
@@ -503,9 +518,14 @@ class _Conv1x1BNFold(torch.autograd.Function):
                                device=x.device)
             nat.gemm_nt(x2, w2, None, running_mean, part)
             vec = nat.bn_finalize(part, weight, bias, running_mean, running_var, momentum, eps, m)
-            yf, keep = nat.gemm_nt_apply(x2, w2, residual_in.permute(0, 2, 3, 1).reshape(m, cout),
-                                         vec[2], vec[3], None if vec_r is None else vec_r[2],
-                                         None if vec_r is None else vec_r[3])
+            if dual is not None:
+                yf, keep = nat.gemm_nt_apply_dual(x2, w2, dual[0], dual[1], vec[2], vec[3],
+                                                  vec_r[2], vec_r[3])
+            else:
+                yf, keep = nat.gemm_nt_apply(x2, w2,
+                                             residual_in.permute(0, 2, 3, 1).reshape(m, cout),
+                                             vec[2], vec[3], None if vec_r is None else vec_r[2],
+                                             None if vec_r is None else vec_r[3])
             y = yf.view(n, h, wd, cout).permute(0, 3, 1, 2)
             z = None
         elif gemm:

@@ -507,7 +507,14 @@ def test_resnet_shortcut_bn_in_epilogue(cuda, monkeypatch):
         calls.append(len(args) > 5 and args[5] is not None)
         return real(*args)
 
+    real_dual = nat.gemm_nt_apply_dual
+
+    def counted_dual(*args):          # the stride-1 shortcut, recomputed in the kernel
+        calls.append(True)
+        return real_dual(*args)
+
     monkeypatch.setattr(nat, "gemm_nt_apply", counted)
+    monkeypatch.setattr(nat, "gemm_nt_apply_dual", counted_dual)
     torch.manual_seed(0)
     base = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
     x = torch.rand(16, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(
@@ -655,3 +662,25 @@ def test_resnet_colsum_from_bn2_apply(cuda, monkeypatch):
         e1 = float((out[True][k] - r).norm()) / nr
         e0 = float((out[False][k] - r).norm()) / nr
         assert e1 <= 1.25 * e0 + 2e-2, (k, e1, e0)
+
+
+@pytest.mark.parametrize("N", [256, 128])
+@pytest.mark.parametrize("M", [1, 64 * 3 + 5, 4096 + 17])
+def test_gemm_nt_apply_dual_matches_materialised(cuda, M, N):
+    """EPI 7 (shortcut conv recomputed inside the apply GEMM) == writing the shortcut conv's
+    output and applying it as an affine residual (EPI 5), bit for bit."""
+    nat = _nat()
+    K = 64
+    assert nat.gemm_apply_dual_supported(N, K) and not nat.gemm_apply_dual_supported(512, 128)
+    g = torch.Generator(device=cuda).manual_seed(M + N + 3)
+    a = torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).to(torch.bfloat16)
+    a2 = torch.randn(M, K, device=cuda, generator=g).to(torch.bfloat16)
+    b2 = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).to(torch.bfloat16)
+    sc, rsc = torch.rand(N, device=cuda, generator=g) + 0.5, torch.rand(N, device=cuda) + 0.5
+    bi, rbi = torch.randn(N, device=cuda, generator=g) * 0.1, torch.randn(N, device=cuda) * 0.1
+    z2 = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    nat.gemm_nt(a2, b2, z2, None, None)
+    y1, m1 = nat.gemm_nt_apply(a, b, z2, sc, bi, rsc, rbi)
+    y2, m2 = nat.gemm_nt_apply_dual(a, b, a2, b2, sc, bi, rsc, rbi)
+    assert torch.equal(y1, y2) and torch.equal(m1, m2)
