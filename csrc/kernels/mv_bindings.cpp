@@ -14,6 +14,7 @@
 #include "mv_bert.h"
 #include "mv_bn.h"
 #include "mv_gemm.h"
+#include "mv_fold.h"
 #include "mv_conv.h"
 #include "mv_kernels.h"
 #include "mv_pool.h"
@@ -915,6 +916,82 @@ void gemm_dual_bias(at::Tensor a1, at::Tensor a2, at::Tensor b, at::Tensor badd,
               "gemm_dual_bias: launch failed");
 }
 
+static void fold_check_f32(const at::Tensor& t, int64_t n, const at::Device& d, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n &&
+                  t.device() == d, "fold: ", what, " must be a contiguous fp32 tensor of ", n,
+              " elements on the GPU");
+}
+
+// {co [5, cout], xsum [cin]}: the BN fold's per-channel coefficients from the consumer's
+// reduce partials part [P, 2, cout], W [cout, cin] (bf16), g = dz^T x [cout, cin] (fp32),
+// the BN's saved vec [4, cout] and gamma; xsum from colsum partials [P2, cin] (or zeros
+// when colsum is None — the caller supplies it)
+std::vector<at::Tensor> fold_coeffs(at::Tensor part, at::Tensor w, at::Tensor g, at::Tensor vec,
+                                    c10::optional<at::Tensor> gamma, int64_t M,
+                                    c10::optional<at::Tensor> colsum) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2,
+              "fold_coeffs: W must be contiguous bf16 [cout, cin]");
+  const int64_t cout = w.size(0), cin = w.size(1);
+  const auto d = w.device();
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.dim() == 3 && part.size(1) == 2 && part.size(2) == cout &&
+                  part.size(0) > 0 && part.device() == d,
+              "fold_coeffs: part must be fp32 [P, 2, cout]");
+  fold_check_f32(g, cout * cin, d, "g");
+  fold_check_f32(vec, 4 * cout, d, "vec");
+  const float* gp = nullptr;
+  if (gamma.has_value() && gamma->defined()) {
+    fold_check_f32(*gamma, cout, d, "gamma");
+    gp = gamma->data_ptr<float>();
+  }
+  const float* cs = nullptr;
+  int P2 = 0;
+  if (colsum.has_value() && colsum->defined()) {
+    TORCH_CHECK(colsum->is_cuda() && colsum->scalar_type() == at::kFloat && colsum->dim() == 2 &&
+                    colsum->size(1) == cin && colsum->stride(1) == 1 && colsum->stride(0) == cin &&
+                    colsum->device() == d,
+                "fold_coeffs: colsum must be fp32 [P2, cin] row-contiguous");
+    cs = colsum->data_ptr<float>();
+    P2 = (int)colsum->size(0);
+  }
+  TORCH_CHECK(M > 0, "fold_coeffs: M must be positive");
+  c10::DeviceGuard guard(d);
+  at::Tensor co = at::empty({5, cout}, part.options());
+  at::Tensor xsum = cs ? at::empty({cin}, part.options()) : at::zeros({cin}, part.options());
+  mv_fold_coeffs(part.data_ptr<float>(), (int)part.size(0), w.data_ptr(), g.data_ptr<float>(),
+                 vec.data_ptr<float>(), gp, M, (int)cout, (int)cin, cs, P2, co.data_ptr<float>(),
+                 xsum.data_ptr<float>(), cur_stream());
+  return {co, xsum};
+}
+
+// {dW bf16 [cout, cin] (undefined if not need_w), bcat bf16 [cin, cout + cin], badd fp32 [cin]}
+std::vector<at::Tensor> fold_products(at::Tensor w, at::Tensor g, c10::optional<at::Tensor> gram,
+                                      at::Tensor co, at::Tensor xsum, bool need_w) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2,
+              "fold_products: W must be contiguous bf16 [cout, cin]");
+  const int64_t cout = w.size(0), cin = w.size(1);
+  TORCH_CHECK(cout % 16 == 0 && cin % 16 == 0 && cout > 0 && cin > 0,
+              "fold_products: channels must be positive multiples of 16 (16x16 tiles)");
+  const auto d = w.device();
+  fold_check_f32(g, cout * cin, d, "g");
+  fold_check_f32(co, 5 * cout, d, "co");
+  fold_check_f32(xsum, cin, d, "xsum");
+  const float* gr = nullptr;
+  if (need_w) {
+    TORCH_CHECK(gram.has_value() && gram->defined(), "fold_products: need_w needs the Gram matrix");
+    fold_check_f32(*gram, cin * cin, d, "gram");
+    gr = gram->data_ptr<float>();
+  }
+  c10::DeviceGuard guard(d);
+  at::Tensor dw = need_w ? at::empty({cout, cin}, w.options()) : at::Tensor();
+  at::Tensor bcat = at::empty({cin, cout + cin}, w.options());
+  at::Tensor badd = at::empty({cin}, co.options());
+  mv_fold_products(w.data_ptr(), g.data_ptr<float>(), gr, co.data_ptr<float>(),
+                   xsum.data_ptr<float>(), (int)cout, (int)cin, need_w ? dw.data_ptr() : nullptr,
+                   bcat.data_ptr(), badd.data_ptr<float>(), cur_stream());
+  return {dw, bcat, badd};
+}
+
 bool gemm_apply_supported(int64_t N, int64_t K) { return mv_gemm_apply_supported((int)N, (int)K); }
 
 // {y, mask}: y = relu(bf16(a . b^T) * scale + bias + res) and its [M, N/8] bitmask (the
@@ -1327,6 +1404,10 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics "
         "(C = None: statistics only)");
   m.def("gemm_apply_supported", &gemm_apply_supported, "gemm_nt_apply handles (N, K)");
+  m.def("fold_coeffs", &fold_coeffs,
+        "{co [5, cout], xsum [cin]}: the BN fold's per-channel coefficients (mv_fold.hip)");
+  m.def("fold_products", &fold_products,
+        "{dW, bcat, badd}: the BN fold's small products (mv_fold.hip)");
   m.def("gemm_apply_dual_supported", &gemm_apply_dual_supported,
         "gemm_nt_apply_dual handles (N, K)");
   m.def("gemm_nt_apply_dual", &gemm_nt_apply_dual,

@@ -38,6 +38,40 @@ _COLSUM = os.environ.get("MIVOD_BN_COLSUM", "1") != "0"
 # MIVOD_BN_SHORTCUT_DUAL=0: a stride-1 shortcut conv's output is written by its statistics
 # GEMM and read back as the residual, instead of being recomputed inside conv3's apply GEMM
 _SHORTCUT_DUAL = os.environ.get("MIVOD_BN_SHORTCUT_DUAL", "1") != "0"
+# MIVOD_BN_FOLD_MATH=0: the fold's per-channel coefficients and small products run as
+# eager PyTorch ops (~22 kernels per block) instead of mv_fold.hip's two kernels
+_FOLD_MATH = os.environ.get("MIVOD_BN_FOLD_MATH", "1") != "0"
+
+
+def _fold_math(nat, wb, g, gram, vec, gamma, m, part, sdz, colsum, xs_fn, need_w):
+    """The BN fold's small-matrix math: (dgamma, dbeta, dW bf16 [cout, cin] or None,
+    bcat bf16 [cin, cout + cin], badd fp32 [cin]) with dx = [dz | x] . bcat^T + badd.
+    ``wb`` = W [cout, cin] bf16, ``g`` = dz^T x, ``gram`` = x^T x (need_w), ``part`` =
+    the consumer's reduce partials (sum dz; or ``sdz`` given), ``colsum`` = [P, cin]
+    column-sum partials of x or None (then ``xs_fn()`` gives colsum(x))."""
+    cout, cin = g.shape
+    if _FOLD_MATH and part is not None:
+        co, xsum = nat.fold_coeffs(part, wb, g, vec, gamma, m, colsum)
+        if need_w and colsum is None:
+            xsum = xs_fn().contiguous()
+        dw, bcat, badd = nat.fold_products(wb, g, gram, co, xsum, need_w)
+        return co[0], co[1], (dw if need_w else None), bcat, badd
+    w2 = wb.float()
+    if sdz is None:
+        sdz = part[:, 0].sum(0)
+    # sum dz (z - mean) = rowdot(W, G) - mean * sum dz, with z = x W^T
+    sdzx = (w2 * g).sum(1) - vec[0] * sdz
+    co = nat.bn_bwd_coeffs(vec, gamma, torch.stack((sdz, sdzx)).unsqueeze(0), m)
+    ca, cb, cc = co[2], co[3], co[4]
+    dw = None
+    if need_w:
+        xs = colsum.sum(0) if colsum is not None else xs_fn()
+        dwf = torch.addcmul(ca[:, None] * g, cb[:, None], w2 @ gram)
+        dwf.addr_(cc, xs)
+        dw = dwf.to(wb.dtype)
+    bcat = torch.cat(((ca[:, None] * w2).t(), w2.t() @ (cb[:, None] * w2)), 1).to(
+        wb.dtype).contiguous()
+    return co[0], co[1], dw, bcat, (cc @ w2).contiguous()
 
 
 def _fusable(x: torch.Tensor, weight) -> bool:
@@ -563,30 +597,22 @@ class _Conv1x1BNFold(torch.autograd.Function):
         nat = K.native()
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         dx = dw = None
-        sdz = None
+        fold_part = None
         if pending is not None and dy is None:
             dz, part = pending
             assert slot.grad is None, "a tapped output has one shortcut consumer"
             n, cin, h, wd = x.shape
             cout, m = w.shape[0], n * h * wd
-            w2 = w.reshape(cout, cin).float()
             x2 = x.permute(0, 2, 3, 1).reshape(m, cin)
             g = nat.wgrad1x1(x, dz, 1, True).view(cout, cin)          # dz^T x
-            # the consumer's epilogue summed dz only: sum dz (z - mean) = rowdot(W, G) -
-            # mean * sum dz, with z = x W^T
-            sdz = part[:, 0].sum(0)
-            sdzx = (w2 * g).sum(1) - vec[0] * sdz
-            co = nat.bn_bwd_coeffs(vec, weight, torch.stack((sdz, sdzx)).unsqueeze(0), m)
-            dg, db, ca, cb, cc = co[0], co[1], co[2], co[3], co[4]
+            gram = nat.wgrad1x1(x, x, 1, True).view(cin, cin) if need_w else None
+            # the consumer's epilogue summed dz only (part); colsum(x) from BN2's apply pass
+            dg, db, dwb, bcat, badd = _fold_math(
+                nat, w.reshape(cout, cin), g, gram, vec, weight, m, part, None, ctx.colsum,
+                lambda: nat.bn_stats(x, None, None, None, None, 0.0, 0.0)[0] * float(m), need_w)
+            fold_part = part
             if need_w:
-                gram = nat.wgrad1x1(x, x, 1, True).view(cin, cin)
-                if ctx.colsum is not None:      # from BN2's apply pass
-                    xs = ctx.colsum.sum(0)
-                else:
-                    xs = nat.bn_stats(x, None, None, None, None, 0.0, 0.0)[0] * float(m)
-                dwf = torch.addcmul(ca[:, None] * g, cb[:, None], w2 @ gram)
-                dwf.addr_(cc, xs)
-                dw = dwf.to(w.dtype).view(cout, cin, 1, 1)
+                dw = dwb.view(cout, cin, 1, 1)
             xs = ctx.xslot
             if (need_x and _FOLD_DX and xs is not None and xs.bn is not None and xs.mode == 1
                     and xs.pending is None and nat.gemm_fold_dx_partials(m, cout, cin) > 0):
@@ -594,19 +620,15 @@ class _Conv1x1BNFold(torch.autograd.Function):
                 # BN2's ReLU backward reduce in its epilogue: BN2 (the producer of x) gets
                 # (d, partials) through its slot and autograd gets None for x
                 zb, _, vec2 = xs.bn
-                bcat = torch.cat(((ca[:, None] * w2).t(), w2.t() @ (cb[:, None] * w2)), 1).to(
-                    x.dtype).contiguous()
                 d = torch.empty_like(zb)
-                part2 = nat.gemm_fold_dx(dz.permute(0, 2, 3, 1).reshape(m, cout), x2, bcat,
-                                         (cc @ w2).contiguous(),
+                part2 = nat.gemm_fold_dx(dz.permute(0, 2, 3, 1).reshape(m, cout), x2, bcat, badd,
                                          d.permute(0, 2, 3, 1).reshape(m, cin),
                                          zb.permute(0, 2, 3, 1).reshape(m, cin), vec2)
                 xs.pending = (d, part2)
             elif need_x:
-                bp = (ca[:, None] * w2).to(x.dtype)
-                q = (w2.t() @ (cb[:, None] * w2)).to(x.dtype)
-                dx2 = torch.addmm((cc @ w2).to(x.dtype), dz.permute(0, 2, 3, 1).reshape(m, cout), bp)
-                dx2.addmm_(x2, q)
+                dx2 = torch.addmm(badd.to(x.dtype), dz.permute(0, 2, 3, 1).reshape(m, cout),
+                                  bcat[:, :cout].t())
+                dx2.addmm_(x2, bcat[:, cout:].t())
                 dx = dx2.view(n, h, wd, cin).permute(0, 3, 1, 2)
         else:
             if z is None:               # recompute forward: rebuild z (same GEMM, same bits)
@@ -642,21 +664,18 @@ class _Conv1x1BNFold(torch.autograd.Function):
             ho, wo = x0s.shape[2], x0s.shape[3]
             mr = nb * ho * wo
             dzc = _cl(dz)
-            wr2 = res_conv_w.reshape(cout_r, c0).float()
             gr = nat.wgrad1x1(x0, dzc, s_r, True).view(cout_r, c0)          # dz^T x0s
-            sdz_r = sdz if sdz is not None else torch.sum(dzc, (0, 2, 3), dtype=torch.float32)
-            sdzx_r = (wr2 * gr).sum(1) - vec_r[0] * sdz_r
-            co_r = nat.bn_bwd_coeffs(vec_r, res_w, torch.stack((sdz_r, sdzx_r)).unsqueeze(0), mr)
-            dgr, dbr, car, cbr, ccr = co_r[0], co_r[1], co_r[2], co_r[3], co_r[4]
-            if ctx.needs_input_grad[14]:
-                gram = nat.wgrad1x1(x0s, x0s, 1, True).view(c0, c0)
-                xsum = nat.bn_stats(x0s, None, None, None, None, 0.0, 0.0)[0] * float(mr)
-                dwf = torch.addcmul(car[:, None] * gr, cbr[:, None], wr2 @ gram)
-                dwf.addr_(ccr, xsum)
-                dwr = dwf.to(res_conv_w.dtype).view(cout_r, c0, 1, 1)
-            bcat = torch.cat(((car[:, None] * wr2).t(), wr2.t() @ (cbr[:, None] * wr2)), 1).to(
-                x0.dtype).contiguous()
-            badd = (ccr @ wr2).contiguous()
+            need_wr = ctx.needs_input_grad[14]
+            gram = nat.wgrad1x1(x0s, x0s, 1, True).view(c0, c0) if need_wr else None
+            # same dz as the main branch: its consumer's partials give sum dz
+            part_r = fold_part
+            sdz_r = None if part_r is not None else torch.sum(dzc, (0, 2, 3), dtype=torch.float32)
+            dgr, dbr, dwrb, bcat, badd = _fold_math(
+                nat, res_conv_w.reshape(cout_r, c0), gr, gram, vec_r, res_w, mr, part_r, sdz_r,
+                None, lambda: nat.bn_stats(x0s, None, None, None, None, 0.0, 0.0)[0] * float(mr),
+                need_wr)
+            if need_wr:
+                dwr = dwrb.view(cout_r, c0, 1, 1)
             dz2d = dzc.permute(0, 2, 3, 1).reshape(mr, cout_r)
             x02d = x0s.permute(0, 2, 3, 1).reshape(mr, c0)
             if nat.gemm_dual_supported(cout_r, c0):

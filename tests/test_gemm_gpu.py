@@ -271,7 +271,14 @@ def test_resnet_bn_fold_matches_unfolded(cuda, monkeypatch):
         calls.append(args[2].shape)
         return real(*args, **kw)
 
+    real_fc = nat.fold_coeffs
+
+    def counted_fc(*args):           # the fused coefficient kernel (ops.bn._FOLD_MATH)
+        calls.append(args[0].shape)
+        return real_fc(*args)
+
     monkeypatch.setattr(nat, "bn_bwd_coeffs", counted)
+    monkeypatch.setattr(nat, "fold_coeffs", counted_fc)
     from mivod.ops import bn as B
     monkeypatch.setattr(B, "_SHORTCUT_FOLD", False)     # counted separately (shortcut test)
     torch.manual_seed(0)
@@ -578,7 +585,14 @@ def test_resnet_shortcut_fold_matches_unfolded(cuda, monkeypatch):
         calls.append(args[2].shape)
         return real(*args)
 
+    real_fc = nat.fold_coeffs
+
+    def counted_fc(*args):
+        calls.append(args[0].shape)
+        return real_fc(*args)
+
     monkeypatch.setattr(nat, "bn_bwd_coeffs", counted)
+    monkeypatch.setattr(nat, "fold_coeffs", counted_fc)
     torch.manual_seed(0)
     base = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
     x = torch.rand(16, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(
@@ -684,3 +698,32 @@ def test_gemm_nt_apply_dual_matches_materialised(cuda, M, N):
     y1, m1 = nat.gemm_nt_apply(a, b, z2, sc, bi, rsc, rbi)
     y2, m2 = nat.gemm_nt_apply_dual(a, b, a2, b2, sc, bi, rsc, rbi)
     assert torch.equal(y1, y2) and torch.equal(m1, m2)
+
+
+@pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256)])
+@pytest.mark.parametrize("colsum", [True, False])
+def test_fold_math_kernels_match_eager(cuda, monkeypatch, cout, cin, colsum):
+    """mv_fold.hip's two kernels == the eager PyTorch composition of the fold's small math."""
+    from mivod.ops import bn as B
+    nat = _nat()
+    g0 = torch.Generator(device=cuda).manual_seed(cout + cin)
+    m = 50000
+    wb = (torch.randn(cout, cin, device=cuda, generator=g0) / cin ** 0.5).to(torch.bfloat16)
+    g = torch.randn(cout, cin, device=cuda, generator=g0) * 10
+    x = torch.randn(m, cin, device=cuda, generator=g0)
+    gram = (x.t() @ x).contiguous()
+    vec = torch.stack((torch.randn(cout, device=cuda, generator=g0) * 0.1,
+                       torch.rand(cout, device=cuda, generator=g0) + 0.5,
+                       torch.randn(cout, device=cuda, generator=g0),
+                       torch.randn(cout, device=cuda, generator=g0))).contiguous()
+    gamma = torch.rand(cout, device=cuda, generator=g0) + 0.5
+    part = torch.randn(37, 2, cout, device=cuda, generator=g0)
+    cs = torch.randn(29, cin, device=cuda, generator=g0) * 5 if colsum else None
+    xs = torch.randn(cin, device=cuda, generator=g0) * 50
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(B, "_FOLD_MATH", on)
+        out[on] = B._fold_math(nat, wb, g, gram, vec, gamma, m, part, None, cs, lambda: xs, True)
+    for a, b, name in zip(out[True], out[False], ("dg", "db", "dw", "bcat", "badd")):
+        torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2 * float(b.abs().max()),
+                                   msg=name)
