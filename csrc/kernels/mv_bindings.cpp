@@ -15,6 +15,7 @@
 #include "mv_bn.h"
 #include "mv_gemm.h"
 #include "mv_fold.h"
+#include "mv_stem.h"
 #include "mv_conv.h"
 #include "mv_kernels.h"
 #include "mv_pool.h"
@@ -992,6 +993,36 @@ std::vector<at::Tensor> fold_products(at::Tensor w, at::Tensor g, c10::optional<
   return {dw, bcat, badd};
 }
 
+// {z [N, 64, 112, 112] channels_last bf16, partial [P, 2, 64]}: the ResNet stem conv
+// (7x7 / 2 / pad 3 on a 4-channel 224x224 NHWC image) with BN statistics around shift
+std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> shift) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 4 &&
+                  x.size(2) == 224 && x.size(3) == 224 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_fwd: x must be a channels_last bf16 [N, 4, 224, 224] GPU tensor");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == 64 &&
+                  w.size(1) == 4 && w.size(2) == 7 && w.size(3) == 7 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.device() == x.device(),
+              "stem_fwd: w must be a channels_last bf16 [64, 4, 7, 7] tensor on x's device");
+  const int64_t N = x.size(0);
+  TORCH_CHECK(N > 0 && N * 112 < (int64_t(1) << 31), "stem_fwd: bad batch");
+  const float* sp = nullptr;
+  if (shift.has_value() && shift->defined()) {
+    TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->is_contiguous() &&
+                    shift->numel() == 64 && shift->device() == x.device(),
+                "stem_fwd: shift must be fp32 [64]");
+    sp = shift->data_ptr<float>();
+  }
+  c10::DeviceGuard guard(x.device());
+  at::Tensor z = at::empty({N, 64, 112, 112},
+                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor part = at::empty({(int64_t)mv_stem_partials((int)N), 2, 64},
+                              x.options().dtype(at::kFloat));
+  mv_stem_fwd(x.data_ptr(), w.data_ptr(), z.data_ptr(), sp, part.data_ptr<float>(), (int)N,
+              cur_stream());
+  return {z, part};
+}
+
 bool gemm_apply_supported(int64_t N, int64_t K) { return mv_gemm_apply_supported((int)N, (int)K); }
 
 // {y, mask}: y = relu(bf16(a . b^T) * scale + bias + res) and its [M, N/8] bitmask (the
@@ -1404,6 +1435,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics "
         "(C = None: statistics only)");
   m.def("gemm_apply_supported", &gemm_apply_supported, "gemm_nt_apply handles (N, K)");
+  m.def("stem_fwd", &stem_fwd,
+        "{z, [P, 2, 64] partials}: ResNet 7x7/2 stem conv on MFMA with BN statistics (mv_stem.hip)");
   m.def("fold_coeffs", &fold_coeffs,
         "{co [5, cout], xsum [cin]}: the BN fold's per-channel coefficients (mv_fold.hip)");
   m.def("fold_products", &fold_products,

@@ -1,0 +1,184 @@
+// ResNet stem: 7x7 / stride 2 / pad 3 conv, 4 (zero-padded RGB) -> 64 channels, NHWC bf16,
+// on MFMA with the stem BatchNorm's statistics in the epilogue.
+//
+// MIOpen runs this shape at ~240 TFLOP/s (2.7 ms per bs-2048 step, K = 7*7*4 is awkward
+// for its tilings) and the BN statistics pass reads the 3.3 GB output again.  Here one
+// output ROW (112 pixels x 64 channels) is an [112 x 224] . [224 x 64] product whose K
+// walks the 7x7 window as (tap row r, tap-column pair, channel): for v_mfma_f32_16x16x32
+// k-step r, the 16-byte operand of k-group g is the input pixels (2p + 2g, 2p + 2g + 1) of
+// padded row r — 8 contiguous bf16 of an LDS image of the 7 input rows — so the im2col
+// operand is read straight from the staged rows (tap column 7 is a zero weight).
+//
+// Workgroup = 4 waves, persistent over output rows (n, oh); wave w owns output channels
+// 16w .. 16w+15 and all 7 pixel tiles.  The filter (64 x 224, XOR-swizzled 16-byte chunks)
+// stays in LDS; the next row's input is prefetched into registers during the MFMAs.
+// Epilogue: bf16 store of 4 consecutive channels per lane + per-channel (sum, sum^2)
+// around the running mean, reduced to one [2][64] partial row per workgroup (fixed order,
+// mv_bn.hip's finalize layout).
+#include "mv_common.h"
+#include "mv_stem.h"
+
+namespace mv {
+namespace stem {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kH = 224, kW = 224, kC = 4, kOH = 112, kOW = 112, kCO = 64;
+constexpr int kPW = 232;                    // padded patch row (230 used: cols -3 .. 226)
+constexpr int kChunks = 32;                 // filter row: 28 used 16-byte chunks, 32 for the swizzle
+constexpr int kPatch = 7 * kPW;             // pixels in the LDS patch
+constexpr int kLoads = (7 * 230 + 255) / 256;   // 8-byte patch loads per thread
+
+__device__ __forceinline__ f32x4v mfma(const bf16x8& a, const bf16x8& b, const f32x4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(256) void stem_fwd_kernel(const __bf16* __restrict__ x,
+                                                       const __bf16* __restrict__ w,
+                                                       __bf16* __restrict__ z,
+                                                       const float* __restrict__ shift,
+                                                       float* __restrict__ partial, int N) {
+  __shared__ __attribute__((aligned(16))) __bf16 ws[kCO * kChunks * 8];   // 32 KB
+  __shared__ __attribute__((aligned(16))) __bf16 ps[kPatch * kC];         // 14.5 KB
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = lane >> 4, rl = lane & 15;
+
+  // filter -> LDS: row o, chunk (r, pair) = w[o][r][2 pair .. 2 pair + 1][0..3] (OHWC)
+  for (int q = tid; q < kCO * kChunks; q += 256) {
+    const int o = q / kChunks, ch = q % kChunks;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (ch < 28) {
+      const int r = ch / 4, pr = ch % 4;
+      const __bf16* src = w + ((o * 7 + r) * 7 + 2 * pr) * kC;
+      const u32x2 a = *reinterpret_cast<const u32x2*>(src);
+      v[0] = a[0];
+      v[1] = a[1];
+      if (pr < 3) {
+        const u32x2 b = *reinterpret_cast<const u32x2*>(src + kC);
+        v[2] = b[0];
+        v[3] = b[1];
+      }
+    }
+    *reinterpret_cast<u32x4*>(ws + (o * kChunks + (ch ^ (o & 7))) * 8) = v;
+  }
+
+  const int64_t rows = (int64_t)N * kOH;
+  u32x2 pre[kLoads];
+  auto gload = [&](int64_t row) {
+    const int n = (int)(row / kOH), oh = (int)(row % kOH);
+#pragma unroll
+    for (int i = 0; i < kLoads; ++i) {
+      const int q = tid + i * 256;
+      const int r = q / 230, pc = q % 230;
+      const int ih = 2 * oh + r - 3, iw = pc - 3;
+      u32x2 v = {0u, 0u};
+      if (q < 7 * 230 && ih >= 0 && ih < kH && iw >= 0 && iw < kW)
+        v = *reinterpret_cast<const u32x2*>(x + (((int64_t)n * kH + ih) * kW + iw) * kC);
+      pre[i] = v;
+    }
+  };
+
+  float sh[4], s1[4], s2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sh[j] = shift ? shift[16 * wv + 4 * g + j] : 0.f;
+    s1[j] = 0.f;
+    s2[j] = 0.f;
+  }
+  int64_t row = blockIdx.x;
+  if (row < rows) gload(row);
+  for (; row < rows; row += gridDim.x) {
+    __syncthreads();                     // previous row's patch reads (and filter stores) done
+#pragma unroll
+    for (int i = 0; i < kLoads; ++i) {
+      const int q = tid + i * 256;
+      if (q < 7 * 230) {
+        const int r = q / 230, pc = q % 230;
+        *reinterpret_cast<u32x2*>(ps + (r * kPW + pc) * kC) = pre[i];
+      }
+    }
+    __syncthreads();
+    if (row + gridDim.x < rows) gload(row + gridDim.x);
+    f32x4v acc[7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) acc[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 7; ++kk) {
+      const int o = 16 * wv + rl, ch = kk * 4 + g;
+      const bf16x8 wf = *reinterpret_cast<const bf16x8*>(ws + (o * kChunks + (ch ^ (o & 7))) * 8);
+#pragma unroll
+      for (int t = 0; t < 7; ++t) {
+        const int p = t * 16 + rl;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ps + (kk * kPW + 2 * p + 2 * g) * kC);
+        acc[t] = mfma(wf, af, acc[t]);
+      }
+    }
+    __bf16* zr = z + row * (int64_t)kOW * kCO + 16 * wv + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+      const int p = t * 16 + rl;
+      const uint32_t lo = cvt_pk_bf16(acc[t][0], acc[t][1]);
+      const uint32_t hi = cvt_pk_bf16(acc[t][2], acc[t][3]);
+      *reinterpret_cast<u32x2*>(zr + (int64_t)p * kCO) = u32x2{lo, hi};
+      const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                          __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[j] - sh[j];
+        s1[j] += d;
+        s2[j] += d * d;
+      }
+    }
+  }
+  // fixed-order reduction over the 16 pixel lanes that share these 4 channels
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      s1[j] += __shfl_xor(s1[j], o, kWave);
+      s2[j] += __shfl_xor(s2[j], o, kWave);
+    }
+  }
+  if (rl == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 16 * wv + 4 * g + j;
+      partial[((int64_t)blockIdx.x * 2 + 0) * kCO + c] = s1[j];
+      partial[((int64_t)blockIdx.x * 2 + 1) * kCO + c] = s2[j];
+    }
+  }
+}
+
+}  // namespace stem
+}  // namespace mv
+
+int mv_stem_partials(int N) {
+  static int per = [] {
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, (const void*)mv::stem::stem_fwd_kernel,
+                                                     256, 0) != hipSuccess || v < 1)
+      v = 1;
+    return v;
+  }();
+  static int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  const int64_t rows = (int64_t)N * mv::stem::kOH;
+  int64_t g = (int64_t)cus * per;
+  if (g > rows) g = rows;
+  return (int)g;
+}
+
+void mv_stem_fwd(const void* x, const void* w, void* z, const float* shift, float* partial, int N,
+                 hipStream_t st) {
+  const int grid = mv_stem_partials(N);
+  hipLaunchKernelGGL(mv::stem::stem_fwd_kernel, dim3(grid), dim3(256), 0, st, (const __bf16*)x,
+                     (const __bf16*)w, (__bf16*)z, shift, partial, N);
+}

@@ -30,6 +30,29 @@ def conv1x1(cin, cout, stride=1):
     return Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 
+class _StemConvStats(torch.autograd.Function):
+    """The stem conv on mivod's MFMA kernel (csrc/kernels/mv_stem.hip) with the following
+    BN's statistics partials from its epilogue; weight gradient on MIOpen's solver."""
+
+    @staticmethod
+    def forward(ctx, x4, w4, shift):
+        from ..ops import kernels as K
+        z, part = K.native().stem_fwd(x4, w4, shift)
+        ctx.save_for_backward(x4, w4)
+        ctx.mark_non_differentiable(part)
+        return z, part
+
+    @staticmethod
+    def backward(ctx, dz, _dpart):
+        x4, w4 = ctx.saved_tensors
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dz = dz.contiguous(memory_format=torch.channels_last)
+            dw = torch.ops.aten.convolution_backward(dz, x4, w4, None, [2, 2], [3, 3], [1, 1],
+                                                     False, [0, 0], 1, [False, True, False])[1]
+        return None, dw, None
+
+
 class StemConv(nn.Conv2d):
     """The 7x7/2 stem conv.  Parameters stay [64, 3, 7, 7]; on the GPU path the
     3-channel NHWC image and the weight are zero-padded to 4 channels first
@@ -37,6 +60,20 @@ class StemConv(nn.Conv2d):
     the stem at ~170 TFLOP/s and need an extra 170 us zero-fill, Cin=4 is ~1.4x
     faster fwd+wgrad (scripts/micro_stem.py).  The zero channel contributes
     nothing, and its weight gradient is sliced away, so the math is unchanged."""
+
+    def forward_stats(self, x, shift):
+        """(conv(x), [P, 2, 64] BN statistics partials around ``shift``) on mivod's stem
+        kernel, or None when it does not apply (MIVOD_STEM_KERNEL=0, not a 224x224 bf16
+        channels_last GPU image, not the ResNet stem geometry)."""
+        if (os.environ.get("MIVOD_STEM_KERNEL", "1") == "0" or not x.is_cuda
+                or x.dtype != torch.bfloat16 or x.dim() != 4 or tuple(x.shape[1:]) != (3, 224, 224)
+                or not x.is_contiguous(memory_format=torch.channels_last)
+                or self.weight.dtype != torch.bfloat16 or tuple(self.weight.shape) != (64, 3, 7, 7)
+                or tuple(self.stride) != (2, 2) or tuple(self.padding) != (3, 3)
+                or self.bias is not None or self.groups != 1 or tuple(self.dilation) != (1, 1)):
+            return None
+        w = F.pad(self.weight, (0, 0, 0, 0, 0, 1)).contiguous(memory_format=torch.channels_last)
+        return _StemConvStats.apply(pad_channels(x, 4), w, shift)
 
     def forward(self, x):
         cp = int(os.environ.get("MIVOD_STEM_CHANNELS", "4"))
@@ -138,7 +175,13 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)   # fused stem
+        r = None
+        if self.bn1.training and self.bn1.track_running_stats:
+            r = self.conv1.forward_stats(x, self.bn1.running_mean)
+        if r is not None:       # stem conv with the BN statistics in its epilogue
+            x = bn_relu_maxpool(r[0], self.bn1, self.maxpool, stats=r[1])
+        else:
+            x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)   # fused stem
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(global_avg_pool(x))
 

@@ -369,9 +369,14 @@ class _BNReluMaxPool(torch.autograd.Function):
     written); backward: gather-form maxpool backward, then BN+ReLU backward."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, slot):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, slot,
+                stats=None):
         nat = K.native()
-        vec = nat.bn_stats(x, weight, bias, running_mean, running_var, momentum, eps)
+        if stats is not None:       # from the stem conv's epilogue (ops.conv.stem_conv_stats)
+            vec = nat.bn_finalize(stats, weight, bias, running_mean, running_var, momentum, eps,
+                                  x.numel() // x.shape[1])
+        else:
+            vec = nat.bn_stats(x, weight, bias, running_mean, running_var, momentum, eps)
         y, idx = nat.maxpool_fwd(x, vec[2], vec[3], True, k, s, p)
         ctx.save_for_backward(x, vec, weight, idx)
         ctx.win, ctx.slot = (k, s, p), slot
@@ -388,7 +393,7 @@ class _BNReluMaxPool(torch.autograd.Function):
         return (dx if ctx.needs_input_grad[0] else None,
                 dg if ctx.needs_input_grad[1] else None,
                 db if ctx.needs_input_grad[2] else None,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 def _pool_args(pool: nn.MaxPool2d):
@@ -404,8 +409,10 @@ def _pool_args(pool: nn.MaxPool2d):
     return (k, s, p) if ok else None
 
 
-def bn_relu_maxpool(x: torch.Tensor, bn: "BatchNorm2d", pool: nn.MaxPool2d) -> torch.Tensor:
-    """``pool(relu(bn(x)))``; fused on GPU in training mode."""
+def bn_relu_maxpool(x: torch.Tensor, bn: "BatchNorm2d", pool: nn.MaxPool2d,
+                    stats=None) -> torch.Tensor:
+    """``pool(relu(bn(x)))``; fused on GPU in training mode.  ``stats``: [P, 2, C]
+    statistics partials of x around the BN's running mean from x's producer."""
     win = _pool_args(pool)
     if (bn.training and bn.track_running_stats and win is not None and
             _fusable(x, bn.weight) and bn.weight is not None):
@@ -415,7 +422,7 @@ def bn_relu_maxpool(x: torch.Tensor, bn: "BatchNorm2d", pool: nn.MaxPool2d) -> t
             momentum = 1.0 / float(bn._mv_steps + int(bn.num_batches_tracked.item()))
         slot = GradSlot()
         y = _BNReluMaxPool.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                 float(momentum), float(bn.eps), *win, slot)
+                                 float(momentum), float(bn.eps), *win, slot, stats)
         y._mv_slot = slot
         return y
     return pool(bn(x, relu=True))

@@ -235,3 +235,77 @@ def test_conv1x1_kernel_matches_fp32(cuda, n, c, k, h, w, s):
     assert torch.equal(y, y2)
     d = y.float().permute(0, 2, 3, 1).reshape(-1, k)
     torch.testing.assert_close(part.sum(0)[0], d.sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_stem_kernel_matches_fp32(cuda, n):
+    """mv_stem.hip: 7x7/2/pad-3 stem conv (4-channel NHWC image) vs fp32 F.conv2d, and its
+    BN-statistics partials vs the statistics of its own bf16 output."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(n)
+    x = torch.rand(n, 4, 224, 224, device=cuda, generator=g)
+    x[:, 3] = 0
+    x = _cl(x.to(torch.bfloat16))
+    w = _cl((torch.randn(64, 4, 7, 7, device=cuda, generator=g) * 0.05).to(torch.bfloat16))
+    shift = torch.randn(64, device=cuda, generator=g) * 0.1
+    z, part = nat.stem_fwd(x, w, shift)
+    assert z.shape == (n, 64, 112, 112) and z.is_contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.float(), w.float(), None, 2, 3)
+    torch.testing.assert_close(z.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    d = (z.float() - shift[None, :, None, None]).permute(1, 0, 2, 3).reshape(64, -1)
+    s = part.sum(0)
+    torch.testing.assert_close(s[0], d.sum(1), rtol=1e-3, atol=1e-1)
+    torch.testing.assert_close(s[1], (d * d).sum(1), rtol=1e-3, atol=1e-1)
+
+
+def test_resnet_stem_kernel_path(cuda, monkeypatch):
+    """ResNet at 224x224 takes the stem kernel (fused BN statistics); every parameter
+    gradient is as close to the fp32 eager reference as the MIOpen stem path's, the stem
+    BN's running statistics match, and the weight gradient of the stem kernel's backward
+    equals F.conv2d's for the same upstream gradient."""
+    import copy
+
+    from mivod.models.resnet import ResNet, _StemConvStats, to_mixed_bf16
+    nat = _nat()
+    calls = []
+    real = nat.stem_fwd
+
+    def counted(*a):
+        calls.append(a[0].shape)
+        return real(*a)
+
+    monkeypatch.setattr(nat, "stem_fwd", counted)
+    torch.manual_seed(0)
+    base = to_mixed_bf16(ResNet((1, 1, 1, 1), num_classes=10)).to(cuda)
+    x = _cl(torch.rand(4, 3, 224, 224, device=cuda).to(torch.bfloat16))
+    tgt = torch.randint(0, 10, (4,), device=cuda)
+
+    def grads(m, inp):
+        F.cross_entropy(m(inp).float(), tgt).backward()
+        return ({k: p.grad.float() for k, p in m.named_parameters()},
+                (m.bn1.running_mean.clone(), m.bn1.running_var.clone()))
+
+    ref, _ = grads(copy.deepcopy(base).float(), x.float())
+    out, st = {}, {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("MIVOD_STEM_KERNEL", on)
+        calls.clear()
+        out[on], st[on] = grads(copy.deepcopy(base), x)
+        assert (len(calls) == 1) == (on == "1"), calls
+    for k, r in ref.items():
+        n = float(r.norm()) + 1e-12
+        e1 = float((out["1"][k] - r).norm()) / n
+        e0 = float((out["0"][k] - r).norm()) / n
+        assert e1 <= 1.25 * e0 + 5e-2, (k, e1, e0)
+    for a, b in zip(st["1"], st["0"]):
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-3)
+    # backward of the kernel path == MIOpen's weight gradient through F.conv2d
+    x4 = _cl(F.pad(x, (0, 0, 0, 0, 0, 1)))
+    w4 = _cl((torch.randn(64, 4, 7, 7, device=cuda) * 0.05).to(torch.bfloat16)).requires_grad_()
+    dz = _cl(torch.randn(4, 64, 112, 112, device=cuda).to(torch.bfloat16))
+    z, _ = _StemConvStats.apply(x4, w4, None)
+    z.backward(dz)
+    g1 = w4.grad.float().clone()
+    w4.grad = None
+    F.conv2d(x4, w4, None, 2, 3).backward(dz)
+    torch.testing.assert_close(g1, w4.grad.float(), rtol=1e-2, atol=1e-2 * float(g1.abs().max()))
