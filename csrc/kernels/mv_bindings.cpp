@@ -776,6 +776,53 @@ at::Tensor maxpool_bwd(at::Tensor dy, c10::optional<at::Tensor> dy2, at::Tensor 
   return dx;
 }
 
+// {dx, dgamma, dbeta}: maxpool(3, 2, 1) backward fused with the backward of the BN+ReLU that
+// produced its input z (ResNet stem): y = the pooled output, vec = the BN's saved [4, C]
+std::vector<at::Tensor> maxpool_bn_bwd(at::Tensor dy, c10::optional<at::Tensor> dy2,
+                                       at::Tensor idx, at::Tensor y, at::Tensor z, at::Tensor vec,
+                                       c10::optional<at::Tensor> gamma) {
+  check_nhwc(dy, "dy");
+  check_nhwc(y, "y");
+  check_nhwc(z, "z");
+  const int64_t N = dy.size(0), C = dy.size(1), OH = dy.size(2), OW = dy.size(3);
+  const int64_t H = z.size(2), W = z.size(3);
+  TORCH_CHECK(y.sizes() == dy.sizes() && z.size(0) == N && z.size(1) == C && H % 2 == 0 &&
+                  W % 2 == 0 && OH == H / 2 && OW == W / 2 && C % 8 == 0 && C <= 256,
+              "maxpool_bn_bwd: needs a 3x3 / 2 / pad-1 pool of an even-sized input, C % 8 == 0, C <= 256");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.is_contiguous() &&
+              idx.numel() == dy.numel(), "maxpool_bn_bwd: idx must be uint8 [N, OH, OW, C]");
+  TORCH_CHECK(N * H * W * (C / 8) < (int64_t(1) << 32), "maxpool_bn_bwd: too large");
+  TORCH_CHECK(vec.is_cuda() && vec.scalar_type() == at::kFloat && vec.is_contiguous() &&
+                  vec.numel() == 4 * C, "maxpool_bn_bwd: saved stats must be fp32 [4, C]");
+  const void* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    check_nhwc(*dy2, "dy2");
+    TORCH_CHECK(dy2->sizes() == dy.sizes(), "maxpool_bn_bwd: dy2 shape");
+    d2 = dy2->data_ptr();
+  }
+  c10::DeviceGuard guard(dy.device());
+  auto fo = dy.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({(int64_t)mv_pool_bn_partials(), 2, C}, fo);
+  mv_pool_bn_reduce(dy.data_ptr(), d2, y.data_ptr(), vec[0].data_ptr<float>(),
+                    vec[2].data_ptr<float>(), vec[3].data_ptr<float>(), part.data_ptr<float>(),
+                    N * OH * OW, (int)C, cur_stream());
+  at::Tensor work = at::empty({5, C}, fo);
+  mv_bn_bwd_from_partials(nullptr, nullptr, nullptr, N * H * W, (int)C, vec[0].data_ptr<float>(),
+                          vec[1].data_ptr<float>(), opt_f32(gamma, C, "weight"),
+                          vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
+                          work[0].data_ptr<float>(), work[1].data_ptr<float>(),
+                          part.data_ptr<float>(), (int)part.size(0), work[2].data_ptr<float>(),
+                          work[3].data_ptr<float>(), work[4].data_ptr<float>(), cur_stream());
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  TORCH_CHECK(mv_maxpool_bn_bwd(dy.data_ptr(), d2, idx.data_ptr<uint8_t>(), z.data_ptr(),
+                                vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
+                                work[2].data_ptr<float>(), work[3].data_ptr<float>(),
+                                work[4].data_ptr<float>(), dx.data_ptr(), (int)N, (int)H, (int)W,
+                                (int)C, (int)OH, (int)OW, cur_stream()),
+              "maxpool_bn_bwd: launch failed");
+  return {dx, work[0], work[1]};
+}
+
 at::Tensor gap_fwd(at::Tensor x) {
   check_nhwc(x, "x");
   c10::DeviceGuard guard(x.device());
@@ -1435,6 +1482,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_nt", &gemm_nt, "C = A . B^T (bf16 MFMA) with optional fused BN statistics "
         "(C = None: statistics only)");
   m.def("gemm_apply_supported", &gemm_apply_supported, "gemm_nt_apply handles (N, K)");
+  m.def("maxpool_bn_bwd", &maxpool_bn_bwd,
+        "{dx, dgamma, dbeta}: maxpool(3,2,1) backward fused with its producer BN+ReLU backward");
   m.def("stem_fwd", &stem_fwd,
         "{z, [P, 2, 64] partials}: ResNet 7x7/2 stem conv on MFMA with BN statistics (mv_stem.hip)");
   m.def("fold_coeffs", &fold_coeffs,

@@ -149,11 +149,24 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restri
 // ow in {b, b+1}, so every lane loads the same 4 windows (no divergent 1/2/4-window
 // loops as in the generic kernel, and each window's dy / index is loaded once per block
 // instead of once per covered pixel) and writes 4 pixels.
+// BN = true: the producing BN+ReLU's backward in the same pass (ResNet stem):
+// dx = ca * relu'(z) * (pooled-gradient sum) + cb * z + cc, with relu'(z) = z * scale + bias > 0
+// and ca, cb, cc from the pooled-level reduce (pool_bn_reduce_kernel + finalize).
+struct PoolBn {
+  const __bf16* z;
+  const float* scale;
+  const float* bias;
+  const float* ca;
+  const float* cb;
+  const float* cc;
+};
+
+template <bool BN>
 __global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(const __bf16* __restrict__ dy,
                                                                const __bf16* __restrict__ dy2,
                                                                const uint8_t* __restrict__ idx,
                                                                __bf16* __restrict__ dx,
-                                                               PoolGeo g) {
+                                                               PoolGeo g, PoolBn pb) {
   const uint32_t cv = (uint32_t)g.C / 8, hb = (uint32_t)g.H / 2, wb = (uint32_t)g.W / 2;
   const uint32_t t = blockIdx.x * 256u + threadIdx.x;
   const uint32_t total = (uint32_t)g.N * hb * wb * cv;
@@ -208,13 +221,92 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(const __bf16* __r
       }
     }
   }
+  float sc[8], bi[8], ka[8], kb[8], kc[8];
+  if constexpr (BN) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = pb.scale[c + e];
+      bi[e] = pb.bias[c + e];
+      ka[e] = pb.ca[c + e];
+      kb[e] = pb.cb[c + e];
+      kc[e] = pb.cc[c + e];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int64_t px = ((int64_t)n * g.H + 2 * a + i) * g.W + 2 * b + jj;
+      if constexpr (BN) {
+        float zv[8];
+        load8_nt(pb.z + px * g.C + c, zv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = __builtin_fmaf(zv[e], sc[e], bi[e]) > 0.f ? acc[i][jj][e] : 0.f;
+          acc[i][jj][e] = ka[e] * d + kb[e] * zv[e] + kc[e];
+        }
+      }
       store8(dx + px * g.C + c, acc[i][jj]);
     }
+}
+
+// Pooled-level reduce of the stem BN+ReLU backward (the partials mv_bn.hip's finalize
+// takes): per pooled window, g = dy + dy2 flows to the window's argmax position p, whose
+// ReLU gate is (y > 0) for the pooled output y = relu(bn(z_p)); so sum d = sum (y > 0) g and
+// sum d (z - mean) = sum (y > 0) g (z_p - mean) with z_p = (y - bias) / scale (y is z_p's
+// BN+ReLU output rounded to bf16: relative error 2^-9 on that factor only).  Reads the
+// pooled tensors (1/4 of the full-resolution ones); fixed-order [P][2][C] partials.
+__global__ __launch_bounds__(256) void pool_bn_reduce_kernel(
+    const __bf16* __restrict__ dy, const __bf16* __restrict__ dy2, const __bf16* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ scale,
+    const float* __restrict__ bias, float* __restrict__ partial, int64_t M, int C) {
+  const int cv = C / 8, rpi = 256 / cv;          // C in {8, 16, ..., 256}: whole rows per block
+  const int tr = threadIdx.x / cv, c = (threadIdx.x % cv) * 8;
+  float s1[8], s2[8], mu[8], isc[8], bi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s1[e] = 0.f;
+    s2[e] = 0.f;
+  }
+  if (tr < rpi) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = mean[c + e];
+      const float scv = scale[c + e];
+      isc[e] = scv != 0.f ? 1.f / scv : 0.f;
+      bi[e] = bias[c + e];
+    }
+    for (int64_t r = (int64_t)blockIdx.x * rpi + tr; r < M; r += (int64_t)gridDim.x * rpi) {
+      float gv[8], yv[8];
+      load8_nt(dy + r * C + c, gv);
+      if (dy2) {
+        float e2[8];
+        load8_nt(dy2 + r * C + c, e2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gv[e] += e2[e];
+      }
+      load8(y + r * C + c, yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = yv[e] > 0.f ? gv[e] : 0.f;
+        s1[e] += d;
+        s2[e] += d * ((yv[e] - bi[e]) * isc[e] - mu[e]);
+      }
+    }
+  }
+  __shared__ float red[2][256 * 8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][threadIdx.x * 8 + e] = s1[e];
+    red[1][threadIdx.x * 8 + e] = s2[e];
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < 2 * C; v += 256) {
+    const int k = v / C, ch = v % C;
+    float s = 0.f;
+    for (int t = 0; t < rpi; ++t) s += red[k][(t * cv + ch / 8) * 8 + ch % 8];
+    partial[((int64_t)blockIdx.x * 2 + k) * C + ch] = s;
+  }
 }
 
 // global average pool: x [N, HW, C] -> y [N, C]; one lane per (n, 8 channels)
@@ -313,8 +405,8 @@ void mv_maxpool_bwd(const void* dy, const void* dy2, const uint8_t* idx, void* d
   if (total >= (int64_t(1) << 32)) return;   // bindings reject such shapes first
   if (k == 3 && s == 2 && p == 1 && H % 2 == 0 && W % 2 == 0 && OH == H / 2 && OW == W / 2) {
     const int64_t t4 = total / 4;
-    hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel, dim3(blocks_for(t4)), dim3(256), 0, st,
-                       (const __bf16*)dy, (const __bf16*)dy2, idx, (__bf16*)dx, g);
+    hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<false>, dim3(blocks_for(t4)), dim3(256), 0, st,
+                       (const __bf16*)dy, (const __bf16*)dy2, idx, (__bf16*)dx, g, PoolBn{});
     return;
   }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
@@ -339,4 +431,28 @@ void mv_pad_channels(const void* x, void* y, int64_t pixels, int cin, int cout, 
   if (!pixels) return;
   hipLaunchKernelGGL(pad_channels_kernel, dim3(blocks_for(pixels)), dim3(256), 0, st,
                      (const uint16_t*)x, (uint16_t*)y, pixels, cin, cout);
+}
+
+int mv_pool_bn_partials() { return 1024; }
+
+void mv_pool_bn_reduce(const void* dy, const void* dy2, const void* y, const float* mean,
+                       const float* scale, const float* bias, float* partial, int64_t M, int C,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(pool_bn_reduce_kernel, dim3(mv_pool_bn_partials()), dim3(256), 0, st,
+                     (const __bf16*)dy, (const __bf16*)dy2, (const __bf16*)y, mean, scale, bias,
+                     partial, M, C);
+}
+
+bool mv_maxpool_bn_bwd(const void* dy, const void* dy2, const uint8_t* idx, const void* z,
+                       const float* scale, const float* bias, const float* ca, const float* cb,
+                       const float* cc, void* dx, int N, int H, int W, int C, int OH, int OW,
+                       hipStream_t st) {
+  PoolGeo g{N, H, W, C, OH, OW, 3, 2, 1};
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  if (!total || total >= (int64_t(1) << 32) || H % 2 || W % 2 || OH != H / 2 || OW != W / 2)
+    return false;
+  PoolBn pb{(const __bf16*)z, scale, bias, ca, cb, cc};
+  hipLaunchKernelGGL(maxpool_bwd_k3s2_kernel<true>, dim3(blocks_for(total / 4)), dim3(256), 0, st,
+                     (const __bf16*)dy, (const __bf16*)dy2, idx, (__bf16*)dx, g, pb);
+  return true;
 }

@@ -41,6 +41,9 @@ _SHORTCUT_DUAL = os.environ.get("MIVOD_BN_SHORTCUT_DUAL", "1") != "0"
 # MIVOD_BN_FOLD_MATH=0: the fold's per-channel coefficients and small products run as
 # eager PyTorch ops (~22 kernels per block) instead of mv_fold.hip's two kernels
 _FOLD_MATH = os.environ.get("MIVOD_BN_FOLD_MATH", "1") != "0"
+# MIVOD_POOL_BN_BWD=0: the stem's maxpool backward writes the pool-input gradient and the
+# BN+ReLU backward runs its own reduce and dx passes over it
+_POOL_BN_BWD = os.environ.get("MIVOD_POOL_BN_BWD", "1") != "0"
 
 
 def _fold_math(nat, wb, g, gram, vec, gamma, m, part, sdz, colsum, xs_fn, need_w):
@@ -378,18 +381,25 @@ class _BNReluMaxPool(torch.autograd.Function):
         else:
             vec = nat.bn_stats(x, weight, bias, running_mean, running_var, momentum, eps)
         y, idx = nat.maxpool_fwd(x, vec[2], vec[3], True, k, s, p)
-        ctx.save_for_backward(x, vec, weight, idx)
+        ctx.save_for_backward(x, vec, weight, idx, y)
         ctx.win, ctx.slot = (k, s, p), slot
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, vec, weight, idx = ctx.saved_tensors
+        x, vec, weight, idx, y = ctx.saved_tensors
         nat = K.native()
         k, s, p = ctx.win
-        dmid = nat.maxpool_bwd(_cl(dy), ctx.slot.take(), idx, x.shape[2], x.shape[3], k, s, p)
         need_affine = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
-        dx, dg, db, _ = nat.bn_bwd(1, dmid, x, None, vec, weight, need_affine, None, 1)
+        if (_POOL_BN_BWD and (k, s, p) == (3, 2, 1) and x.shape[2] % 2 == 0
+                and x.shape[3] % 2 == 0 and y.shape[2] * 2 == x.shape[2]
+                and y.shape[3] * 2 == x.shape[3] and x.shape[1] <= 256):
+            # the BN+ReLU backward fused into the pool backward: reduce over the pooled
+            # tensors, then one full-resolution pass (no intermediate pool gradient)
+            dx, dg, db = nat.maxpool_bn_bwd(_cl(dy), ctx.slot.take(), idx, y, x, vec, weight)
+        else:
+            dmid = nat.maxpool_bwd(_cl(dy), ctx.slot.take(), idx, x.shape[2], x.shape[3], k, s, p)
+            dx, dg, db, _ = nat.bn_bwd(1, dmid, x, None, vec, weight, need_affine, None, 1)
         return (dx if ctx.needs_input_grad[0] else None,
                 dg if ctx.needs_input_grad[1] else None,
                 db if ctx.needs_input_grad[2] else None,

@@ -2,6 +2,8 @@
 PyTorch references: fused BN-affine+ReLU+maxpool forward/backward (uint8
 argmax, gather backward, second gradient stream), global average pool, BN
 backward with dy2, and a whole ResNet-50 step fused vs eager."""
+import copy
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -206,3 +208,32 @@ def test_bn_bwd_bitmask_mode_equals_saved_output_mode(cuda, shape, stride):
         ref = nat.bn_bwd(2, dy, x, y, vec, g, True, dy2, stride)
         for a, c in zip(got, ref):
             assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("n,c,h", [(2, 64, 16), (3, 16, 10), (1, 256, 8)])
+def test_maxpool_bn_bwd_fused_matches_unfused(cuda, monkeypatch, n, c, h):
+    """Stem backward: maxpool(3,2,1) backward fused with the producer BN+ReLU backward
+    (pooled-level reduce + one full-resolution pass) == maxpool_bwd then bn_bwd(mode 1)."""
+    from mivod.ops import bn as B
+    torch.manual_seed(n + c)
+    bn = B.BatchNorm2d(c).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = (torch.randn(n, c, h, h, device=cuda) * 2).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    out = {}
+    g = None
+    for on in (True, False):
+        monkeypatch.setattr(B, "_POOL_BN_BWD", on)
+        xi = x.clone().requires_grad_()
+        b = copy.deepcopy(bn)
+        y = B.bn_relu_maxpool(xi, b, pool)
+        if g is None:
+            g = torch.randn_like(y.float()).to(torch.bfloat16)
+        y.backward(g)
+        out[on] = (y.float(), xi.grad.float(), b.weight.grad.float(), b.bias.grad.float())
+    assert torch.equal(out[True][0], out[False][0])
+    for a, r in zip(out[True][1:], out[False][1:]):
+        torch.testing.assert_close(a, r, rtol=2e-2, atol=2e-2 * float(r.abs().max()) + 1e-3)
