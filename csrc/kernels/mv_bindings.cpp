@@ -1410,7 +1410,8 @@ at::Tensor wgrad3x3(at::Tensor x, at::Tensor dy, int64_t stride) {
 }
 
 // weight gradient of y = conv1x1(x, w, stride, pad 0): dw [K, C, 1, 1] bf16
-at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride, bool fp32_out) {
+at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride, bool fp32_out,
+                    c10::optional<at::Tensor> dy2) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "wgrad1x1: x must be a channels_last bf16 GPU tensor");
@@ -1418,9 +1419,20 @@ at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride, bool fp32_out) 
                   dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.device() == x.device(),
               "wgrad1x1: dy must be a channels_last bf16 tensor on x's device");
   TORCH_CHECK(stride == 1 || stride == 2, "wgrad1x1: stride must be 1 or 2");
-  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K1 = dy.size(1);
   const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   TORCH_CHECK(dy.size(0) == N && dy.size(2) == Ho && dy.size(3) == Wo, "wgrad1x1: dy shape");
+  // dy2: a second dy stream stacked below dy's channels (dw = [dy | dy2]^T . x)
+  const bool two = dy2.has_value() && dy2->defined();
+  int64_t K = K1;
+  if (two) {
+    TORCH_CHECK(dy2->is_cuda() && dy2->scalar_type() == at::kBFloat16 && dy2->dim() == 4 &&
+                    dy2->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    dy2->device() == x.device() && dy2->size(0) == N && dy2->size(2) == Ho &&
+                    dy2->size(3) == Wo && dy2->size(1) % 64 == 0,
+                "wgrad1x1: dy2 must be a channels_last bf16 [N, K2, Ho, Wo] tensor");
+    K = K1 + dy2->size(1);
+  }
   TORCH_CHECK(C % 64 == 0 && K % 64 == 0 && N * H * W * std::max(C, K) < (int64_t(1) << 40),
               "wgrad1x1: channels must be multiples of 64");
   c10::DeviceGuard guard(x.device());
@@ -1431,7 +1443,7 @@ at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride, bool fp32_out) 
                             at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(mv_wgrad1x1(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), work.data_ptr<float>(),
                           (int)N, (int)H, (int)W, (int)C, (int)K, (int)stride, cur_stream(),
-                          fp32_out),
+                          fp32_out, two ? dy2->data_ptr() : nullptr, (int)K1),
               "wgrad1x1: unsupported shape");
   return dw;
 }
@@ -1526,7 +1538,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("conv3x3_bn_bwd", &conv3x3_bn_bwd,
         "stride-1 3x3 data gradient with the producing BN+ReLU's backward reduce fused");
   m.def("wgrad1x1", &wgrad1x1, "1x1 (pad 0, stride 1/2) conv weight gradient on MFMA",
-        py::arg("x"), py::arg("dy"), py::arg("stride") = 1, py::arg("fp32_out") = false);
+        py::arg("x"), py::arg("dy"), py::arg("stride") = 1, py::arg("fp32_out") = false,
+        py::arg("dy2") = py::none());
   m.def("wgrad3x3", &wgrad3x3, "3x3 (pad 1) conv weight gradient on MFMA (transposed LDS reads)",
         py::arg("x"), py::arg("dy"), py::arg("stride") = 1);
   m.def("conv3x3_partials", &conv3x3_partials, "partial rows of conv3x3's statistics epilogue");

@@ -31,5 +31,7 @@ bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, in
 // given dy; work: fp32 [mv_wgrad1x1_workspace(M, K, C)], M = N * Ho * Wo
 int64_t mv_wgrad1x1_workspace(int64_t M, int K, int C);
 // (dw_fp32: dw is fp32 instead of bf16)
+// dy2 != null: dy's channels [k1, K) come from dy2 ([N, Ho, Wo, K - k1]) — dw = [dy | dy2]^T . x
 bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
-                 int K, int stride, hipStream_t st, bool dw_fp32 = false);
+                 int K, int stride, hipStream_t st, bool dw_fp32 = false,
+                 const void* dy2 = nullptr, int k1 = 0);

@@ -60,6 +60,10 @@ struct Geo {
   int H, W, C, Ho, Wo, K, st;
   int64_t M;
   int ks = 3;        // filter size: 3 (pad 1) or 1 (pad 0) for the forward kernel
+  // wgrad1x1 only: dy channels [k1, K) come from dy2 ([M, K - k1], output rows) — the BN
+  // fold's dz^T x and Gram x^T x in one pass over x (k1 = K: single source)
+  const __bf16* dy2 = nullptr;
+  int k1 = 0;
 };
 
 // per-thread state of the A rows it stages (A_CH rows, fixed source chunk): the byte
@@ -708,8 +712,11 @@ __attribute__((amdgpu_waves_per_eu(FK == 2 ? 2 : 1))) void wgrad1x1_kernel(
       const int j = i * HPW + hg;                 // sub-tile (thread-group uniform)
       const int ws = WS == 1 ? 0 : j / SUB, r = j % SUB;
       const bool in = mrow[ws] < g.M;
-      const void* src = r < KS ? (const void*)(DY + mrow[ws] * g.K + k0 + r * 64 + sch * 8)
-                               : (const void*)(X + xrow[ws] * g.C + c0 + (r - KS) * 64 + sch * 8);
+      const int kk = k0 + r * 64;                 // sub-tile uniform: one source per sub-tile
+      const void* src =
+          r >= KS ? (const void*)(X + xrow[ws] * g.C + c0 + (r - KS) * 64 + sch * 8)
+          : kk < g.k1 ? (const void*)(DY + mrow[ws] * g.k1 + kk + sch * 8)
+                      : (const void*)(g.dy2 + mrow[ws] * (g.K - g.k1) + (kk - g.k1) + sch * 8);
       glds16(in ? src : (const void*)zaddr, stg + j * WG_TILE);
     }
   };
@@ -856,10 +863,16 @@ int64_t mv_wgrad1x1_workspace(int64_t M, int K, int C) {
 }
 
 bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
-                 int K, int stride, hipStream_t st, bool dw_fp32) {
+                 int K, int stride, hipStream_t st, bool dw_fp32, const void* dy2, int k1) {
   using namespace mv::conv;
   if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2)) return false;
   Geo g;
+  g.dy2 = (const __bf16*)dy2;
+  g.k1 = dy2 ? k1 : K;
+  if (dy2) {     // each staged k block must come from one source
+    const W1Cfg c = w1_cfg(K, C);
+    if (k1 <= 0 || k1 >= K || k1 % (64 * c.wk * c.fk) != 0) return false;
+  }
   g.H = H;
   g.W = W;
   g.C = C;

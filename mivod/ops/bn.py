@@ -44,6 +44,8 @@ _FOLD_MATH = os.environ.get("MIVOD_BN_FOLD_MATH", "1") != "0"
 # MIVOD_POOL_BN_BWD=0: the stem's maxpool backward writes the pool-input gradient and the
 # BN+ReLU backward runs its own reduce and dx passes over it
 _POOL_BN_BWD = os.environ.get("MIVOD_POOL_BN_BWD", "1") != "0"
+# MIVOD_BN_DUAL_WGRAD=0: the fold's dz^T x and Gram x^T x as two wgrad1x1 launches
+_DUAL_WGRAD = os.environ.get("MIVOD_BN_DUAL_WGRAD", "1") != "0"
 
 
 def _fold_math(nat, wb, g, gram, vec, gamma, m, part, sdz, colsum, xs_fn, need_w):
@@ -621,8 +623,13 @@ class _Conv1x1BNFold(torch.autograd.Function):
             n, cin, h, wd = x.shape
             cout, m = w.shape[0], n * h * wd
             x2 = x.permute(0, 2, 3, 1).reshape(m, cin)
-            g = nat.wgrad1x1(x, dz, 1, True).view(cout, cin)          # dz^T x
-            gram = nat.wgrad1x1(x, x, 1, True).view(cin, cin) if need_w else None
+            if need_w and _DUAL_WGRAD:
+                # dz^T x and the Gram x^T x in one pass over x: [dz | x]^T . x
+                gg = nat.wgrad1x1(x, dz, 1, True, x).view(cout + cin, cin)
+                g, gram = gg[:cout], gg[cout:]
+            else:
+                g = nat.wgrad1x1(x, dz, 1, True).view(cout, cin)          # dz^T x
+                gram = nat.wgrad1x1(x, x, 1, True).view(cin, cin) if need_w else None
             # the consumer's epilogue summed dz only (part); colsum(x) from BN2's apply pass
             dg, db, dwb, bcat, badd = _fold_math(
                 nat, w.reshape(cout, cin), g, gram, vec, weight, m, part, None, ctx.colsum,
@@ -681,9 +688,13 @@ class _Conv1x1BNFold(torch.autograd.Function):
             ho, wo = x0s.shape[2], x0s.shape[3]
             mr = nb * ho * wo
             dzc = _cl(dz)
-            gr = nat.wgrad1x1(x0, dzc, s_r, True).view(cout_r, c0)          # dz^T x0s
             need_wr = ctx.needs_input_grad[14]
-            gram = nat.wgrad1x1(x0s, x0s, 1, True).view(c0, c0) if need_wr else None
+            if need_wr and _DUAL_WGRAD:      # [dz | x0s]^T . x0s (x0 read at the stride)
+                gg = nat.wgrad1x1(x0, dzc, s_r, True, x0s).view(cout_r + c0, c0)
+                gr, gram = gg[:cout_r], gg[cout_r:]
+            else:
+                gr = nat.wgrad1x1(x0, dzc, s_r, True).view(cout_r, c0)          # dz^T x0s
+                gram = nat.wgrad1x1(x0s, x0s, 1, True).view(c0, c0) if need_wr else None
             # same dz as the main branch: its consumer's partials give sum dz
             part_r = fold_part
             sdz_r = None if part_r is not None else torch.sum(dzc, (0, 2, 3), dtype=torch.float32)

@@ -309,3 +309,20 @@ def test_resnet_stem_kernel_path(cuda, monkeypatch):
     w4.grad = None
     F.conv2d(x4, w4, None, 2, 3).backward(dz)
     torch.testing.assert_close(g1, w4.grad.float(), rtol=1e-2, atol=1e-2 * float(g1.abs().max()))
+
+
+@pytest.mark.parametrize("n,c,k,h,s", [(2, 64, 256, 9, 1), (2, 128, 512, 8, 1), (1, 256, 512, 10, 2),
+                                       (1, 256, 1024, 7, 1)])
+def test_wgrad1x1_dual_dy(cuda, n, c, k, h, s):
+    """wgrad1x1 with a second dy stream: [dy | dy2]^T . x == the two products stacked."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(n + c + k)
+    x = _cl(torch.randn(n, c, h, h, device=cuda, generator=g).to(torch.bfloat16))
+    ho = (h - 1) // s + 1
+    dy = _cl(torch.randn(n, k, ho, ho, device=cuda, generator=g).to(torch.bfloat16))
+    dy2 = _cl(torch.randn(n, c, ho, ho, device=cuda, generator=g).to(torch.bfloat16))
+    both = nat.wgrad1x1(x, dy, s, True, dy2).view(k + c, c)
+    a = nat.wgrad1x1(x, dy, s, True).view(k, c)
+    b = nat.wgrad1x1(x, dy2, s, True).view(c, c)
+    ref = torch.cat((a, b))
+    torch.testing.assert_close(both, ref, rtol=1e-4, atol=1e-3 * float(ref.abs().max()))
