@@ -22,6 +22,11 @@ from . import kernels as K
 _BN_MASK = os.environ.get("MIVOD_BN_MASK", "1") != "0"
 # MIVOD_BN_RECOMPUTE=0: the BN3 fold materialises z and runs the separate apply pass (A/B)
 _RECOMPUTE = os.environ.get("MIVOD_BN_RECOMPUTE", "1") != "0"
+# ... for K = Cin <= MIVOD_BN_RECOMPUTE_MAXK (default 128): at K = 256 (ResNet-50 layer3) the
+# second GEMM's compute (~0.4 ms at bs 2048) is about what the z write + read saves (bench A/B
+# 128 vs 256: 15,294 / 15,330 vs 15,304 / 15,282 img/s, level); blocks with a projection
+# shortcut keep it (its BN is applied in that epilogue)
+_RECOMPUTE_MAXK = int(os.environ.get("MIVOD_BN_RECOMPUTE_MAXK", "128"))
 # MIVOD_BN_FOLD_DX=0: the fold's data gradient runs as two hipBLASLt GEMMs and BN2 runs its
 # own backward reduce pass, instead of mv_gemm's dual-source kernel with that reduce fused
 _FOLD_DX = os.environ.get("MIVOD_BN_FOLD_DX", "1") != "0"
@@ -558,7 +563,8 @@ class _Conv1x1BNFold(torch.autograd.Function):
             residual_in = zr_in
         else:
             residual_in, dual = residual, None
-        if gemm and _RECOMPUTE and nat.gemm_apply_supported(cout, cin):
+        if (gemm and _RECOMPUTE and nat.gemm_apply_supported(cout, cin)
+                and (res_cfg is not None or cin <= _RECOMPUTE_MAXK)):
             # z is never materialised: a statistics-only GEMM pass, the finalize, then the
             # GEMM again with relu(bn(z) + residual) and the bitmask in its epilogue (the
             # same tile order, so z and y are bit-identical to the two-pass path).  The
