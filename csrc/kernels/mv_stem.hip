@@ -9,8 +9,8 @@
 // padded row r — 8 contiguous bf16 of an LDS image of the 7 input rows — so the im2col
 // operand is read straight from the staged rows (tap column 7 is a zero weight).
 //
-// Workgroup = 4 waves, persistent over output rows (n, oh); wave w owns output channels
-// 16w .. 16w+15 and all 7 pixel tiles.  The filter (64 x 224, XOR-swizzled 16-byte chunks)
+// Workgroup = 4 waves, persistent over pairs of output rows (n, oh..oh+1); wave w owns output
+// channels 16w .. 16w+15 and all 2 x 7 pixel tiles.  The filter (64 x 224, XOR-swizzled 16-byte chunks)
 // stays in LDS; the next row's input is prefetched into registers during the MFMAs.
 // Epilogue: bf16 store of 4 consecutive channels per lane + per-channel (sum, sum^2)
 // around the running mean, reduced to one [2][64] partial row per workgroup (fixed order,
@@ -29,8 +29,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kH = 224, kW = 224, kC = 4, kOH = 112, kOW = 112, kCO = 64;
 constexpr int kPW = 232;                    // padded patch row (230 used: cols -3 .. 226)
 constexpr int kChunks = 32;                 // filter row: 28 used 16-byte chunks, 32 for the swizzle
-constexpr int kPatch = 7 * kPW;             // pixels in the LDS patch
-constexpr int kLoads = (7 * 230 + 255) / 256;   // 8-byte patch loads per thread
+// R output rows per iteration share 2R + 5 staged input rows (R = 2: 9 rows for 2 output
+// rows instead of 14, and each filter fragment feeds 14 pixel tiles)
+#ifndef MV_STEM_ROWS
+#define MV_STEM_ROWS 2
+#endif
+constexpr int kR = MV_STEM_ROWS;
+constexpr int kIR = 2 * kR + 5;             // staged input rows
+constexpr int kPatch = kIR * kPW;           // pixels in the LDS patch
+constexpr int kLoads = (kIR * 230 + 255) / 256;   // 8-byte patch loads per thread
 
 __device__ __forceinline__ f32x4v mfma(const bf16x8& a, const bf16x8& b, const f32x4v& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -65,17 +72,17 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const __bf16* __restrict_
     *reinterpret_cast<u32x4*>(ws + (o * kChunks + (ch ^ (o & 7))) * 8) = v;
   }
 
-  const int64_t rows = (int64_t)N * kOH;
+  const int64_t rows = (int64_t)N * (kOH / kR);      // row groups
   u32x2 pre[kLoads];
   auto gload = [&](int64_t row) {
-    const int n = (int)(row / kOH), oh = (int)(row % kOH);
+    const int n = (int)(row / (kOH / kR)), oh = (int)(row % (kOH / kR)) * kR;
 #pragma unroll
     for (int i = 0; i < kLoads; ++i) {
       const int q = tid + i * 256;
       const int r = q / 230, pc = q % 230;
       const int ih = 2 * oh + r - 3, iw = pc - 3;
       u32x2 v = {0u, 0u};
-      if (q < 7 * 230 && ih >= 0 && ih < kH && iw >= 0 && iw < kW)
+      if (q < kIR * 230 && ih >= 0 && ih < kH && iw >= 0 && iw < kW)
         v = *reinterpret_cast<const u32x2*>(x + (((int64_t)n * kH + ih) * kW + iw) * kC);
       pre[i] = v;
     }
@@ -95,41 +102,48 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const __bf16* __restrict_
 #pragma unroll
     for (int i = 0; i < kLoads; ++i) {
       const int q = tid + i * 256;
-      if (q < 7 * 230) {
+      if (q < kIR * 230) {
         const int r = q / 230, pc = q % 230;
         *reinterpret_cast<u32x2*>(ps + (r * kPW + pc) * kC) = pre[i];
       }
     }
     __syncthreads();
     if (row + gridDim.x < rows) gload(row + gridDim.x);
-    f32x4v acc[7];
+    f32x4v acc[kR][7];
 #pragma unroll
-    for (int t = 0; t < 7; ++t) acc[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < kR; ++j)
+#pragma unroll
+      for (int t = 0; t < 7; ++t) acc[j][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < 7; ++kk) {
       const int o = 16 * wv + rl, ch = kk * 4 + g;
       const bf16x8 wf = *reinterpret_cast<const bf16x8*>(ws + (o * kChunks + (ch ^ (o & 7))) * 8);
 #pragma unroll
-      for (int t = 0; t < 7; ++t) {
-        const int p = t * 16 + rl;
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ps + (kk * kPW + 2 * p + 2 * g) * kC);
-        acc[t] = mfma(wf, af, acc[t]);
-      }
+      for (int j = 0; j < kR; ++j)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+          const int p = t * 16 + rl;
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(
+              ps + ((2 * j + kk) * kPW + 2 * p + 2 * g) * kC);
+          acc[j][t] = mfma(wf, af, acc[j][t]);
+        }
     }
-    __bf16* zr = z + row * (int64_t)kOW * kCO + 16 * wv + 4 * g;
+#pragma unroll
+    for (int j = 0; j < kR; ++j)
 #pragma unroll
     for (int t = 0; t < 7; ++t) {
+      __bf16* zr = z + (row * kR + j) * (int64_t)kOW * kCO + 16 * wv + 4 * g;
       const int p = t * 16 + rl;
-      const uint32_t lo = cvt_pk_bf16(acc[t][0], acc[t][1]);
-      const uint32_t hi = cvt_pk_bf16(acc[t][2], acc[t][3]);
+      const uint32_t lo = cvt_pk_bf16(acc[j][t][0], acc[j][t][1]);
+      const uint32_t hi = cvt_pk_bf16(acc[j][t][2], acc[j][t][3]);
       *reinterpret_cast<u32x2*>(zr + (int64_t)p * kCO) = u32x2{lo, hi};
       const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                           __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d = v[j] - sh[j];
-        s1[j] += d;
-        s2[j] += d * d;
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[e] - sh[e];
+        s1[e] += d;
+        s2[e] += d * d;
       }
     }
   }
@@ -170,7 +184,7 @@ int mv_stem_partials(int N) {
       v = 256;
     return v;
   }();
-  const int64_t rows = (int64_t)N * mv::stem::kOH;
+  const int64_t rows = (int64_t)N * (mv::stem::kOH / mv::stem::kR);
   int64_t g = (int64_t)cus * per;
   if (g > rows) g = rows;
   return (int)g;
