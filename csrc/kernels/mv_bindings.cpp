@@ -1070,6 +1070,27 @@ std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w, c10::optional<at::T
   return {z, part};
 }
 
+// dw [64, 4, 7, 7] channels_last bf16: the stem conv's weight gradient (mv_stem.hip)
+at::Tensor stem_wgrad(at::Tensor x, at::Tensor dz) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 4 &&
+                  x.size(2) == 224 && x.size(3) == 224 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_wgrad: x must be a channels_last bf16 [N, 4, 224, 224] GPU tensor");
+  const int64_t N = x.size(0);
+  TORCH_CHECK(dz.is_cuda() && dz.scalar_type() == at::kBFloat16 && dz.dim() == 4 &&
+                  dz.size(0) == N && dz.size(1) == 64 && dz.size(2) == 112 && dz.size(3) == 112 &&
+                  dz.is_contiguous(at::MemoryFormat::ChannelsLast) && dz.device() == x.device(),
+              "stem_wgrad: dz must be a channels_last bf16 [N, 64, 112, 112] tensor on x's device");
+  TORCH_CHECK(N > 0 && N * 112 < (int64_t(1) << 31), "stem_wgrad: bad batch");
+  c10::DeviceGuard guard(x.device());
+  at::Tensor work = at::empty({(int64_t)mv_stem_wgrad_blocks((int)N) * 64 * 224},
+                              x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({64, 4, 7, 7}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  mv_stem_wgrad(x.data_ptr(), dz.data_ptr(), dw.data_ptr(), work.data_ptr<float>(), (int)N,
+                cur_stream());
+  return dw;
+}
+
 bool gemm_apply_supported(int64_t N, int64_t K) { return mv_gemm_apply_supported((int)N, (int)K); }
 
 // {y, mask}: y = relu(bf16(a . b^T) * scale + bias + res) and its [M, N/8] bitmask (the
@@ -1496,6 +1517,7 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_apply_supported", &gemm_apply_supported, "gemm_nt_apply handles (N, K)");
   m.def("maxpool_bn_bwd", &maxpool_bn_bwd,
         "{dx, dgamma, dbeta}: maxpool(3,2,1) backward fused with its producer BN+ReLU backward");
+  m.def("stem_wgrad", &stem_wgrad, "ResNet stem conv weight gradient on MFMA (mv_stem.hip)");
   m.def("stem_fwd", &stem_fwd,
         "{z, [P, 2, 64] partials}: ResNet 7x7/2 stem conv on MFMA with BN statistics (mv_stem.hip)");
   m.def("fold_coeffs", &fold_coeffs,

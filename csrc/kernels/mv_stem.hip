@@ -196,3 +196,144 @@ void mv_stem_fwd(const void* x, const void* w, void* z, const float* shift, floa
   hipLaunchKernelGGL(mv::stem::stem_fwd_kernel, dim3(grid), dim3(256), 0, st, (const __bf16*)x,
                      (const __bf16*)w, (__bf16*)z, shift, partial, N);
 }
+
+// ---------------------------------------------------------------- weight gradient
+// dW[o][k] = sum over output pixels p of dz[p][o] * patch_p[k], k = (tap row r, tap column
+// s in 0..7, channel c) — s = 7 is dropped at the end.  Per output row: dz [112 x 64] staged
+// in LDS (rows 112..127 zero, the XOR layout of mv_conv's transposed reads) and the 7 input
+// rows; both MFMA operands are pixel(k)-major and come from gfx950 transposed LDS reads —
+// for the image operand the "row" of pixel p is the 16 contiguous values patch[r][2p + s0 ..
+// 2p + s0 + 3][0..3] (row pitch 16 bytes, overlapping rows).  Wave w owns output channels
+// 16w..16w+15 and all 14 k tiles; fp32 partials [G][64][224] + a fixed-order reduce.
+namespace mv {
+namespace stem {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int dswz(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
+
+// 4 pixels (rows r0 .. r0+3) of column col0 + c of the [128][64] dz tile
+__device__ __forceinline__ s16x4 dz_tr4(const __bf16* base, int r0, int col0, int c) {
+  const int r = r0 + (c >> 2), e = col0 + 4 * (c & 3);
+  const __bf16* p = base + r * 64 + (((e >> 3) ^ dswz(r)) << 3) + (e & 7);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+}
+
+// 4 pixels (p0 .. p0+3, clamped to 111) of k column c of tile (r, s0) of the patch
+__device__ __forceinline__ s16x4 px_tr4(const __bf16* ps, int p0, int r, int s0, int c) {
+  int p = p0 + (c >> 2);
+  p = p < kOW - 1 ? p : kOW - 1;
+  const __bf16* a = ps + (r * kPW + 2 * p + s0) * kC + 4 * (c & 3);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a);
+}
+
+__device__ __forceinline__ bf16x8 cat8(const s16x4& a, const s16x4& b) {
+  bf16x8 o;
+  short* q = reinterpret_cast<short*>(&o);
+  q[0] = a[0]; q[1] = a[1]; q[2] = a[2]; q[3] = a[3];
+  q[4] = b[0]; q[5] = b[1]; q[6] = b[2]; q[7] = b[3];
+  return o;
+}
+
+constexpr int kWLoads = (7 * 230 + 255) / 256;   // 8-byte patch loads per thread (one row)
+
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(const __bf16* __restrict__ x,
+                                                         const __bf16* __restrict__ dz,
+                                                         float* __restrict__ partial, int N) {
+  __shared__ __attribute__((aligned(16))) __bf16 ps[7 * kPW * kC];        // 13 KB
+  __shared__ __attribute__((aligned(16))) __bf16 ds[128 * 64];            // 16 KB
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = lane >> 4, cl = lane & 15;
+  const int64_t rows = (int64_t)N * kOH;
+  f32x4v acc[14];
+#pragma unroll
+  for (int t = 0; t < 14; ++t) acc[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  // dz rows 112..127 stay zero (written once)
+  for (int q = tid; q < 16 * 8; q += 256) {
+    const int r = 112 + q / 8, ch = q % 8;
+    *reinterpret_cast<u32x4*>(ds + r * 64 + ((ch ^ dswz(r)) << 3)) = u32x4{0u, 0u, 0u, 0u};
+  }
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int n = (int)(row / kOH), oh = (int)(row % kOH);
+    __syncthreads();                        // previous row's LDS reads done
+#pragma unroll
+    for (int i = 0; i < kWLoads; ++i) {
+      const int q = tid + i * 256;
+      if (q < 7 * 230) {
+        const int r = q / 230, pc = q % 230;
+        const int ih = 2 * oh + r - 3, iw = pc - 3;
+        u32x2 v = {0u, 0u};
+        if (ih >= 0 && ih < kH && iw >= 0 && iw < kW)
+          v = *reinterpret_cast<const u32x2*>(x + (((int64_t)n * kH + ih) * kW + iw) * kC);
+        *reinterpret_cast<u32x2*>(ps + (r * kPW + pc) * kC) = v;
+      }
+    }
+    const __bf16* dzr = dz + row * (int64_t)kOW * kCO;
+    for (int q = tid; q < kOW * 8; q += 256) {
+      const int r = q / 8, ch = q % 8;
+      *reinterpret_cast<u32x4*>(ds + r * 64 + ((ch ^ dswz(r)) << 3)) =
+          *reinterpret_cast<const u32x4*>(dzr + r * 64 + ch * 8);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int p0 = ks * 32 + 8 * g;
+      const bf16x8 af = cat8(dz_tr4(ds, p0, 16 * wv, cl), dz_tr4(ds, p0 + 4, 16 * wv, cl));
+#pragma unroll
+      for (int t = 0; t < 14; ++t) {
+        const int r = t >> 1, s0 = 4 * (t & 1);
+        const bf16x8 bf = cat8(px_tr4(ps, p0, r, s0, cl), px_tr4(ps, p0 + 4, r, s0, cl));
+        acc[t] = mfma(af, bf, acc[t]);
+      }
+    }
+  }
+  float* pb = partial + (int64_t)blockIdx.x * kCO * 224;
+#pragma unroll
+  for (int t = 0; t < 14; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pb[(16 * wv + 4 * g + r) * 224 + t * 16 + cl] = acc[t][r];
+}
+
+// dw[o][r][s][c] (OHWC, s < 7) = sum_g partial[g][o][r * 32 + s * 4 + c], fixed order
+__global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ partial,
+                                                                int G, __bf16* __restrict__ dw) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= kCO * 7 * 7 * kC) return;
+  const int c = i % kC, s = (i / kC) % 7, r = (i / (kC * 7)) % 7, o = i / (kC * 49);
+  const int k = r * 32 + s * 4 + c;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int gi = 0;
+  for (; gi + 3 < G; gi += 4) {
+    a0 += partial[((int64_t)gi * kCO + o) * 224 + k];
+    a1 += partial[((int64_t)(gi + 1) * kCO + o) * 224 + k];
+    a2 += partial[((int64_t)(gi + 2) * kCO + o) * 224 + k];
+    a3 += partial[((int64_t)(gi + 3) * kCO + o) * 224 + k];
+  }
+  for (; gi < G; ++gi) a0 += partial[((int64_t)gi * kCO + o) * 224 + k];
+  dw[i] = (__bf16)((a0 + a1) + (a2 + a3));
+}
+
+}  // namespace stem
+}  // namespace mv
+
+int mv_stem_wgrad_blocks(int N) {
+  static int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  int64_t g = (int64_t)cus * 4;
+  const int64_t rows = (int64_t)N * mv::stem::kOH;
+  if (g > rows) g = rows;
+  return (int)g;
+}
+
+void mv_stem_wgrad(const void* x, const void* dz, void* dw, float* work, int N, hipStream_t st) {
+  const int G = mv_stem_wgrad_blocks(N);
+  hipLaunchKernelGGL(mv::stem::stem_wgrad_kernel, dim3(G), dim3(256), 0, st, (const __bf16*)x,
+                     (const __bf16*)dz, work, N);
+  hipLaunchKernelGGL(mv::stem::stem_wgrad_reduce_kernel, dim3((64 * 196 + 255) / 256), dim3(256), 0,
+                     st, work, G, (__bf16*)dw);
+}

@@ -32,7 +32,8 @@ def conv1x1(cin, cout, stride=1):
 
 class _StemConvStats(torch.autograd.Function):
     """The stem conv on mivod's MFMA kernel (csrc/kernels/mv_stem.hip) with the following
-    BN's statistics partials from its epilogue; weight gradient on MIOpen's solver."""
+    BN's statistics partials from its epilogue; weight gradient on mv_stem.hip's kernel too
+    (opt-in MIVOD_STEM_WGRAD=1 until measured; default MIOpen)."""
 
     @staticmethod
     def forward(ctx, x4, w4, shift):
@@ -48,8 +49,13 @@ class _StemConvStats(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             dz = dz.contiguous(memory_format=torch.channels_last)
-            dw = torch.ops.aten.convolution_backward(dz, x4, w4, None, [2, 2], [3, 3], [1, 1],
-                                                     False, [0, 0], 1, [False, True, False])[1]
+            if os.environ.get("MIVOD_STEM_WGRAD", "0") == "1":
+                from ..ops import kernels as K
+                dw = K.native().stem_wgrad(x4, dz)
+            else:
+                dw = torch.ops.aten.convolution_backward(dz, x4, w4, None, [2, 2], [3, 3], [1, 1],
+                                                         False, [0, 0], 1,
+                                                         [False, True, False])[1]
         return None, dw, None
 
 

@@ -326,3 +326,21 @@ def test_wgrad1x1_dual_dy(cuda, n, c, k, h, s):
     b = nat.wgrad1x1(x, dy2, s, True).view(c, c)
     ref = torch.cat((a, b))
     torch.testing.assert_close(both, ref, rtol=1e-4, atol=1e-3 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_stem_wgrad_kernel_matches_miopen(cuda, n):
+    """mv_stem.hip weight gradient vs MIOpen's (fp32-accumulated) for the same dz."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(10 + n)
+    x = torch.rand(n, 4, 224, 224, device=cuda, generator=g)
+    x[:, 3] = 0
+    x = _cl(x.to(torch.bfloat16))
+    w = _cl((torch.randn(64, 4, 7, 7, device=cuda, generator=g) * 0.05).to(torch.bfloat16))
+    dz = _cl(torch.randn(n, 64, 112, 112, device=cuda, generator=g).to(torch.bfloat16))
+    dw = nat.stem_wgrad(x, dz)
+    assert dw.shape == (64, 4, 7, 7) and dw.is_contiguous(memory_format=torch.channels_last)
+    ref = torch.ops.aten.convolution_backward(dz.float(), x.float(), w.float(), None, [2, 2],
+                                              [3, 3], [1, 1], False, [0, 0], 1,
+                                              [False, True, False])[1]
+    torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
