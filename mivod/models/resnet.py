@@ -33,7 +33,7 @@ def conv1x1(cin, cout, stride=1):
 class _StemConvStats(torch.autograd.Function):
     """The stem conv on mivod's MFMA kernel (csrc/kernels/mv_stem.hip) with the following
     BN's statistics partials from its epilogue; weight gradient on mv_stem.hip's kernel too
-    (opt-in MIVOD_STEM_WGRAD=1 until measured; default MIOpen)."""
+    (opt-in MIVOD_STEM_WGRAD=1: correct but slower than MIOpen so far — bench A/B 15,235-15,263 vs 15,360-15,385 img/s; no prefetch, one row per barrier pair)."""
 
     @staticmethod
     def forward(ctx, x4, w4, shift):
