@@ -253,28 +253,51 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const __bf16* __restric
     const int r = 112 + q / 8, ch = q % 8;
     *reinterpret_cast<u32x4*>(ds + r * 64 + ((ch ^ dswz(r)) << 3)) = u32x4{0u, 0u, 0u, 0u};
   }
-  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+  // next row's patch and dz in registers while the current row computes
+  constexpr int kDz = (kOW * 8 + 255) / 256;   // 16-byte dz chunks per thread
+  u32x2 pp[kWLoads];
+  u32x4 pd[kDz];
+  auto gload = [&](int64_t row) {
     const int n = (int)(row / kOH), oh = (int)(row % kOH);
+#pragma unroll
+    for (int i = 0; i < kWLoads; ++i) {
+      const int q = tid + i * 256;
+      const int r = q / 230, pc = q % 230;
+      const int ih = 2 * oh + r - 3, iw = pc - 3;
+      u32x2 v = {0u, 0u};
+      if (q < 7 * 230 && ih >= 0 && ih < kH && iw >= 0 && iw < kW)
+        v = *reinterpret_cast<const u32x2*>(x + (((int64_t)n * kH + ih) * kW + iw) * kC);
+      pp[i] = v;
+    }
+    const __bf16* dzr = dz + row * (int64_t)kOW * kCO;
+#pragma unroll
+    for (int i = 0; i < kDz; ++i) {
+      const int q = tid + i * 256;
+      pd[i] = q < kOW * 8 ? *reinterpret_cast<const u32x4*>(dzr + q * 8) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  int64_t row = blockIdx.x;
+  if (row < rows) gload(row);
+  for (; row < rows; row += gridDim.x) {
     __syncthreads();                        // previous row's LDS reads done
 #pragma unroll
     for (int i = 0; i < kWLoads; ++i) {
       const int q = tid + i * 256;
       if (q < 7 * 230) {
         const int r = q / 230, pc = q % 230;
-        const int ih = 2 * oh + r - 3, iw = pc - 3;
-        u32x2 v = {0u, 0u};
-        if (ih >= 0 && ih < kH && iw >= 0 && iw < kW)
-          v = *reinterpret_cast<const u32x2*>(x + (((int64_t)n * kH + ih) * kW + iw) * kC);
-        *reinterpret_cast<u32x2*>(ps + (r * kPW + pc) * kC) = v;
+        *reinterpret_cast<u32x2*>(ps + (r * kPW + pc) * kC) = pp[i];
       }
     }
-    const __bf16* dzr = dz + row * (int64_t)kOW * kCO;
-    for (int q = tid; q < kOW * 8; q += 256) {
-      const int r = q / 8, ch = q % 8;
-      *reinterpret_cast<u32x4*>(ds + r * 64 + ((ch ^ dswz(r)) << 3)) =
-          *reinterpret_cast<const u32x4*>(dzr + r * 64 + ch * 8);
+#pragma unroll
+    for (int i = 0; i < kDz; ++i) {
+      const int q = tid + i * 256;
+      if (q < kOW * 8) {
+        const int r = q / 8, ch = q % 8;
+        *reinterpret_cast<u32x4*>(ds + r * 64 + ((ch ^ dswz(r)) << 3)) = pd[i];
+      }
     }
     __syncthreads();
+    if (row + gridDim.x < rows) gload(row + gridDim.x);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int p0 = ks * 32 + 8 * g;

@@ -33,7 +33,8 @@ def conv1x1(cin, cout, stride=1):
 class _StemConvStats(torch.autograd.Function):
     """The stem conv on mivod's MFMA kernel (csrc/kernels/mv_stem.hip) with the following
     BN's statistics partials from its epilogue; weight gradient on mv_stem.hip's kernel too
-    (opt-in MIVOD_STEM_WGRAD=1: correct but slower than MIOpen so far — bench A/B 15,235-15,263 vs 15,360-15,385 img/s; no prefetch, one row per barrier pair)."""
+    (MIVOD_STEM_WGRAD=0: MIOpen's solver; bench A/B 15,290/15,312 vs 15,278/15,240 img/s with
+    the next row prefetched into registers — without the prefetch it was 0.8% behind)."""
 
     @staticmethod
     def forward(ctx, x4, w4, shift):
@@ -49,7 +50,7 @@ class _StemConvStats(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             dz = dz.contiguous(memory_format=torch.channels_last)
-            if os.environ.get("MIVOD_STEM_WGRAD", "0") == "1":
+            if os.environ.get("MIVOD_STEM_WGRAD", "1") != "0":
                 from ..ops import kernels as K
                 dw = K.native().stem_wgrad(x4, dz)
             else:

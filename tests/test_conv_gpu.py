@@ -308,7 +308,7 @@ def test_resnet_stem_kernel_path(cuda, monkeypatch):
     g1 = w4.grad.float().clone()
     w4.grad = None
     F.conv2d(x4, w4, None, 2, 3).backward(dz)
-    torch.testing.assert_close(g1, w4.grad.float(), rtol=1e-2, atol=1e-2 * float(g1.abs().max()))
+    torch.testing.assert_close(g1, w4.grad.float(), rtol=2e-2, atol=2e-2 * float(g1.abs().max()))
 
 
 @pytest.mark.parametrize("n,c,k,h,s", [(2, 64, 256, 9, 1), (2, 128, 512, 8, 1), (1, 256, 512, 10, 2),
