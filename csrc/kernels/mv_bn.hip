@@ -688,12 +688,13 @@ void mv_bn_fwd_from_partials(const void* x, const void* res, void* y, int64_t M,
   if (y) mv_bn_apply(x, res, y, M, C, scale, bias, relu, st, mask);
 }
 
-// apply / dx passes: 2 rows in flight per lane; MIVOD_BN_APPLY_U=4 selects 4 (measured
-// equal on the bs512 shapes, scripts/micro_bn.py)
+// apply / dx passes: 4 rows in flight per lane (ResNet-50 bs2048 bench A/B, two boxes:
+// +0.2% / +0.4% over 2; equal on the bs512 shapes, scripts/micro_bn.py);
+// MIVOD_BN_APPLY_U=2 selects 2
 static bool apply_u2() {
   static const bool on = [] {
     const char* e = std::getenv("MIVOD_BN_APPLY_U");
-    return !(e && e[0] == '4');
+    return e && e[0] == '2';
   }();
   return on;
 }
