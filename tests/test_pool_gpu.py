@@ -17,7 +17,8 @@ def _cl(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
-@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 16, 9, 13), (3, 8, 7, 8), (2, 16, 8, 10)])
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 16, 9, 13), (3, 8, 7, 8), (2, 16, 8, 10),
+                                   (2, 8, 12, 16)])
 @pytest.mark.parametrize("affine", [True, False])
 @pytest.mark.parametrize("with_dy2", [False, True])
 def test_maxpool_matches_torch(cuda, shape, affine, with_dy2):
