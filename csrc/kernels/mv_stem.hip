@@ -43,6 +43,9 @@ __device__ __forceinline__ f32x4v mfma(const bf16x8& a, const bf16x8& b, const f
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// NOTE (round 2): __launch_bounds__(256, 2) compiles this kernel to 236 VGPRs with the MFMA
+// accumulators in VGPRs (2 waves/SIMD, 1.21 vs 1.53 ms) but produced wrong outputs (NaN)
+// in test_stem_kernel_matches_fp32 on gfx950 — not understood yet; kept at 1 wave/SIMD.
 __global__ __launch_bounds__(256) void stem_fwd_kernel(const __bf16* __restrict__ x,
                                                        const __bf16* __restrict__ w,
                                                        __bf16* __restrict__ z,
