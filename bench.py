@@ -21,9 +21,14 @@ over ``MIVOD_TRANSPORT=gloo-gpu``, since RCCL refuses two ranks on one GPU).
 
 Data: synthetic, generated on the GPU once (uniform images, random labels);
 weights: random init.  Rank 0 prints ONE JSON line, with a ``comm`` record:
-gradient buckets, bytes per step, collectives per step and the exposed
+gradient buckets, bytes per step, collectives per step, the exposed
 communication time (comm-stream work still running after backward's last
-kernel was enqueued, per step).
+kernel was enqueued, per step), the MEASURED allreduce time per step with
+per-bucket algorithm / bus bandwidth (timing events around every bucket
+collective on the comm stream), and what RCCL itself sees (run-time and header
+version, ncclCommCount, CTA range).  Multi-rank runs default the RCCL watchdog
+and stall-shutdown timeouts (mivod.utils.benchutil) so a hang exits non-zero
+with the stuck collective's name.
 """
 from __future__ import annotations
 
@@ -115,6 +120,37 @@ def self_launch(argv, nproc: int, script: str = None) -> int:
     return launch(slots, cmd, extra, tag_output=False)
 
 
+def make_record(args, size: int, ips: float, ms: float, transport: str, comm: dict) -> dict:
+    """The ONE JSON line rank 0 prints (driver contract + BASELINE.json metric)."""
+    return {
+        "metric": BASELINE_METRIC,
+        "value": round(ips, 2),
+        "unit": "images/sec",
+        "n_gpus": size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (on-device uniform images, random labels; random-init weights)",
+        "config": {
+            "model": "ResNet-50",
+            "global_batch": args.batch * size,
+            "per_gpu_batch": args.batch,
+            "seq_len": None,
+            "image": args.image,
+            "parallelism": f"dp{size}",
+            "optimizer": f"mivod Fused{args.optimizer.upper()} via DistributedOptimizer",
+            "compression": args.compression,
+            "transport": transport,
+            "hip_graph": bool(args.graph),
+        },
+        "comm": comm,
+    }
+
+
 def _launched() -> bool:
     return any(k in os.environ for k in ("WORLD_SIZE", "HOROVOD_RANK", "OMPI_COMM_WORLD_RANK"))
 
@@ -125,6 +161,9 @@ def main():
         sys.exit(self_launch(sys.argv[1:], args.gpus))
     import torch
     import torch.nn.functional as F
+
+    from mivod.utils import benchutil as BU
+    BU.multi_rank_defaults()        # multi-rank: a stuck collective ends the job with a diagnosis
 
     import mivod.torch as hvd
     from mivod.models.resnet import resnet50, to_mixed_bf16
@@ -208,6 +247,9 @@ def main():
         return loss
 
     run = step if args.graph else timed_step
+    timed_comm = not args.graph and getattr(opt, "_mvd_comm", False)
+    if timed_comm:
+        opt.time_comm(True)          # timing events around every bucket collective
     stats0 = C.gpu_stats()
     C.barrier()
     torch.cuda.synchronize()
@@ -225,6 +267,7 @@ def main():
     grad_bytes = sum(nb for _, nb, _ in plan)
     exposed = [max(0.0, a.elapsed_time(b)) for a, b in timing] if timing else []
     calls = (stats1.get("calls", 0) - stats0.get("calls", 0)) / max(args.steps, 1)
+    measured = BU.comm_timing_record(opt.comm_timings() if timed_comm else [], args.steps, size)
     comm = {
         "buckets": len(plan),
         "grad_bytes_per_step": grad_bytes,
@@ -232,38 +275,14 @@ def main():
         "collectives_per_step": round(calls, 2),
         "exposed_comm_ms": round(sum(exposed) / len(exposed), 3) if exposed else None,
         "exposed_comm_ms_max": round(max(exposed), 3) if exposed else None,
+        **measured,
+        "rccl": BU.rccl_info(),
     }
     if rank == 0:
         print(f"[bench] warmup {args.warmup} steps {warm_s:.1f}s; loss {float(loss.detach()):.4f}; "
               f"{ms:.2f} ms/step; buckets={len(opt.bucket_plan())}; peak HBM "
               f"{torch.cuda.max_memory_allocated(dev) / 2**30:.1f} GiB", file=sys.stderr)
-        rec = {
-            "metric": BASELINE_METRIC,
-            "value": round(ips, 2),
-            "unit": "images/sec",
-            "n_gpus": size,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (on-device uniform images, random labels; random-init weights)",
-            "config": {
-                "model": "ResNet-50",
-                "global_batch": args.batch * size,
-                "per_gpu_batch": args.batch,
-                "seq_len": None,
-                "image": args.image,
-                "parallelism": f"dp{size}",
-                "optimizer": f"mivod Fused{args.optimizer.upper()} via DistributedOptimizer",
-                "compression": args.compression,
-                "transport": _transport(size),
-                "hip_graph": bool(args.graph),
-            },
-            "comm": comm,
-        }
+        rec = make_record(args, size, ips, ms, _transport(size), comm)
         print(json.dumps(rec), flush=True)
     hvd.shutdown()
 

@@ -71,6 +71,9 @@ def main():
 
     import torch
 
+    from mivod.utils import benchutil as BU
+    BU.multi_rank_defaults()        # multi-rank: a stuck collective ends the job with a diagnosis
+
     import mivod.torch as hvd
     from mivod.models.bert import BertConfig, BertForPreTraining, synthetic_batch
     from mivod.optim import FusedAdam
@@ -117,6 +120,9 @@ def main():
             print(f"[bert] first step {time.perf_counter() - t0:.1f}s", file=sys.stderr,
                   flush=True)
     torch.cuda.synchronize()
+    timed_comm = getattr(opt, "_mvd_comm", False)
+    if timed_comm:
+        opt.time_comm(True)          # timing events around every bucket collective
     stats0 = C.gpu_stats()
     C.barrier()
     torch.cuda.synchronize()
@@ -133,7 +139,9 @@ def main():
             "collectives_per_step": round((stats1.get("calls", 0) - stats0.get("calls", 0))
                                           / max(args.steps, 1), 2),
             "exposed_comm_ms": round(sum(exposed) / len(exposed), 3) if exposed else None,
-            "guard": opt.guard_stats()}
+            "guard": opt.guard_stats(),
+            **BU.comm_timing_record(opt.comm_timings() if timed_comm else [], args.steps, size),
+            "rccl": BU.rccl_info()}
     if rank == 0:
         print(json.dumps({
             "metric": "sequences/sec (whole node), BERT-Large bf16 pre-training, fp16 compression + Adasum",

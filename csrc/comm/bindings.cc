@@ -14,6 +14,8 @@ PYBIND11_MODULE(_mvcomm, m) {
   m.doc() = "mivod GPU data plane: RCCL communicator, collectives on the comm stream, watchdog";
   m.def("unique_id", [] { return py::bytes(unique_id()); });
   m.def("rccl_version", &rccl_version);
+  m.def("header_version", [] { return (int)NCCL_VERSION_CODE; });
+  m.def("version_note", &version_note);
 
   // ncclDataType_t / ncclRedOp_t codes (rccl.h)
   m.attr("INT8") = (int)ncclInt8;
@@ -53,6 +55,7 @@ PYBIND11_MODULE(_mvcomm, m) {
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("size", &Comm::size)
       .def_property_readonly("device", &Comm::device)
+      .def("count", &Comm::count)
       .def("allreduce",
            [](Comm& c, uintptr_t in, uintptr_t out, size_t n, int dt, int op, uintptr_t s) {
              c.allreduce((const void*)in, (void*)out, n, dt, op, s);
@@ -99,10 +102,11 @@ PYBIND11_MODULE(_mvcomm, m) {
       .def("stats", &Comm::stats)
       .def("outstanding", &Comm::outstanding);
 
-  // xGMI mesh one-shot allreduce over HIP-IPC-mapped peer staging buffers
+  // xGMI mesh allreduce (one-shot / two-shot) over HIP-IPC-mapped peer buffers
   py::class_<Mesh>(m, "Mesh")
-      .def(py::init<int, int, int, size_t>(), py::arg("rank"), py::arg("size"),
-           py::arg("device"), py::arg("capacity_bytes"))
+      .def(py::init<int, int, int, size_t, double, bool>(), py::arg("rank"), py::arg("size"),
+           py::arg("device"), py::arg("capacity_bytes"), py::arg("timeout_s") = 30.0,
+           py::arg("exit_on_timeout") = true)
       .def("handles", [](const Mesh& me) { return py::bytes(me.handles()); })
       .def("open",
            [](Mesh& me, std::vector<py::bytes> hs) {
@@ -111,16 +115,22 @@ PYBIND11_MODULE(_mvcomm, m) {
              py::gil_scoped_release nogil;
              me.open(v);
            })
+      .def("stage_ptr", &Mesh::stage_ptr)
       .def("allreduce",
-           [](Mesh& me, uintptr_t in, uintptr_t out, size_t n, int dt, float scale, uintptr_t s) {
-             me.allreduce((const void*)in, (void*)out, n, dt, scale, s);
-           },
-           py::call_guard<py::gil_scoped_release>())
-      .def("status", &Mesh::status, py::call_guard<py::gil_scoped_release>())
+           [](Mesh& me, uintptr_t in, uintptr_t out, size_t n, int dt, float scale, uintptr_t s,
+              int algo) { me.allreduce((const void*)in, (void*)out, n, dt, scale, s, algo); },
+           py::arg("inp"), py::arg("out"), py::arg("count"), py::arg("dtype"), py::arg("scale"),
+           py::arg("stream"), py::arg("algo") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("status", &Mesh::status)
+      .def("failed", &Mesh::failed)
       .def("close", &Mesh::close, py::call_guard<py::gil_scoped_release>())
+      .def_property("oneshot_max_bytes", &Mesh::oneshot_max_bytes, &Mesh::set_oneshot_max_bytes)
       .def_property_readonly("capacity", &Mesh::capacity)
+      .def_property_readonly("timeout_s", &Mesh::timeout_s)
       .def_property_readonly("rank", &Mesh::rank)
       .def_property_readonly("size", &Mesh::size)
       .def_property_readonly("calls", &Mesh::calls)
-      .def_property_readonly("bytes", &Mesh::bytes);
+      .def_property_readonly("bytes", &Mesh::bytes)
+      .def_property_readonly("copies_saved", &Mesh::copies_saved)
+      .def_property_readonly("two_shot_calls", &Mesh::two_shot_calls);
 }

@@ -40,9 +40,37 @@ int rccl_version() {
   return v;
 }
 
+// NCCL_VERSION(X,Y,Z) codes are X*10000 + Y*100 + Z from 2.9 on
+static int major_minor(int code) { return code / 100; }
+
+std::string version_note() {
+  const int rt = rccl_version();
+  if (major_minor(rt) == major_minor(NCCL_VERSION_CODE)) return "";
+  return "RCCL run-time library " + std::to_string(rt) + " != header " +
+         std::to_string(NCCL_VERSION_CODE) +
+         " (mivod links the librccl PyTorch loads; version-dependent features are gated on "
+         "the run-time version)";
+}
+
+bool runtime_has_ctas_config() { return rccl_version() >= 21700; }
+bool runtime_has_fp8() { return rccl_version() >= 22400; }
+
+int Comm::count() const {
+  int n = 0;
+  MV_NCCL(ncclCommCount(comm_, &n));
+  return n;
+}
+
 size_t Comm::dtype_size(int dtype) {
   switch (dtype) {
-    case ncclInt8: case ncclUint8: case ncclFloat8e4m3: case ncclFloat8e5m2: return 1;
+    case ncclInt8: case ncclUint8: return 1;
+    case ncclFloat8e4m3: case ncclFloat8e5m2:
+      // the enum codes of the header; an older run-time library reads them as
+      // something else (or rejects them)
+      if (!runtime_has_fp8())
+        throw std::invalid_argument("mivod RCCL: fp8 needs RCCL >= 2.24 at run time (have " +
+                                    std::to_string(rccl_version()) + ")");
+      return 1;
     case ncclFloat16: case ncclBfloat16: return 2;
     case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
     case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
@@ -60,6 +88,11 @@ Comm::Comm(const std::string& uid, int rank, int size, int device, double timeou
   ncclUniqueId id;
   std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
   MV_HIP(hipSetDevice(device));
+  if ((min_ctas > 0 || max_ctas > 0) && !runtime_has_ctas_config()) {
+    fprintf(stderr, "[mivod] RCCL %d has no ncclConfig_t CTA range; using the default\n",
+            rccl_version());
+    min_ctas = max_ctas = min_ctas_ = max_ctas_ = 0;
+  }
   if (min_ctas > 0 || max_ctas > 0) {
     // CTA (= channel) range of this communicator: how many xGMI rings a collective
     // spreads over (the RCCL autotune in mivod/parallel/autotune.py sweeps it)

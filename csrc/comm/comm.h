@@ -33,6 +33,12 @@ namespace mvcomm {
 
 std::string unique_id();   // 128 raw bytes (NCCL_UNIQUE_ID_BYTES)
 int rccl_version();
+// "" when the RCCL library loaded at run time matches the header this module was
+// compiled against (major.minor), else a one-line description of the skew
+std::string version_note();
+// features gated on the run-time library version (not the header's)
+bool runtime_has_ctas_config();   // ncclConfig_t minCTAs / maxCTAs (NCCL >= 2.17)
+bool runtime_has_fp8();           // ncclFloat8e4m3 / e5m2 codes 10 / 11 (NCCL >= 2.24)
 
 struct CommStats {
   int64_t calls = 0;
@@ -57,6 +63,8 @@ class Comm {
   int max_ctas() const { return max_ctas_; }
   int size() const { return size_; }
   int device() const { return device_; }
+  // ncclCommCount: the number of ranks RCCL itself sees in this communicator
+  int count() const;
 
   // op: ncclRedOp_t value (ncclSum/ncclProd/ncclMax/ncclMin/ncclAvg).
   void allreduce(const void* in, void* out, size_t count, int dtype, int op, uintptr_t stream);

@@ -108,6 +108,16 @@ void flat_cast(at::Tensor src, at::Tensor dst, double scale, c10::optional<at::T
                       (float)scale, nf_ptr(nonfinite), cur_stream());
 }
 
+void nonfinite_scan(at::Tensor x, at::Tensor flag) {
+  check_flat(x, "x");
+  TORCH_CHECK(flag.is_cuda() && flag.scalar_type() == at::kInt && flag.numel() >= 1 &&
+                  flag.device() == x.device() && flag.is_contiguous(),
+              "nonfinite_scan: flag must be an int32 GPU tensor on x's device");
+  c10::DeviceGuard guard(x.device());
+  mv_launch_nonfinite_scan(x.data_ptr(), dtype_code(x), x.numel(), flag.data_ptr<int>(),
+                           cur_stream());
+}
+
 void check_master(const at::Tensor& g, const at::Tensor& t, const char* what) {
   check_flat(t, what);
   TORCH_CHECK(t.scalar_type() == at::kFloat, what, " must be fp32");
@@ -1042,7 +1052,8 @@ std::vector<at::Tensor> fold_products(at::Tensor w, at::Tensor g, c10::optional<
 
 // {z [N, 64, 112, 112] channels_last bf16, partial [P, 2, 64]}: the ResNet stem conv
 // (7x7 / 2 / pad 3 on a 4-channel 224x224 NHWC image) with BN statistics around shift
-std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> shift) {
+std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> shift,
+                                 int64_t grid) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 4 &&
                   x.size(2) == 224 && x.size(3) == 224 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -1063,10 +1074,13 @@ std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w, c10::optional<at::T
   c10::DeviceGuard guard(x.device());
   at::Tensor z = at::empty({N, 64, 112, 112},
                            x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  at::Tensor part = at::empty({(int64_t)mv_stem_partials((int)N), 2, 64},
-                              x.options().dtype(at::kFloat));
+  // grid > 0: a non-default persistent grid (tests); any size >= 1 is valid — the
+  // kernel's row loop and the partial rows follow the grid
+  TORCH_CHECK(grid >= 0 && grid <= (int64_t(1) << 20), "stem_fwd: bad grid");
+  const int g = grid > 0 ? (int)grid : mv_stem_partials((int)N);
+  at::Tensor part = at::empty({(int64_t)g, 2, 64}, x.options().dtype(at::kFloat));
   mv_stem_fwd(x.data_ptr(), w.data_ptr(), z.data_ptr(), sp, part.data_ptr<float>(), (int)N,
-              cur_stream());
+              cur_stream(), g);
   return {z, part};
 }
 
@@ -1471,12 +1485,23 @@ at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride, bool fp32_out,
 
 }  // namespace
 
+// A tensor over device memory mivod owns elsewhere (the mesh's IPC staging
+// slot): no copy, no deleter — the owner outlives every view by construction.
+at::Tensor tensor_from_ptr(uintptr_t ptr, int64_t numel, at::ScalarType dtype, int64_t device) {
+  TORCH_CHECK(ptr != 0 && numel >= 0, "tensor_from_ptr: bad pointer / size");
+  TORCH_CHECK(ptr % 16 == 0, "tensor_from_ptr: pointer must be 16-byte aligned");
+  return torch::from_blob(reinterpret_cast<void*>(ptr), {numel},
+                          at::TensorOptions().dtype(dtype).device(at::kCUDA, device));
+}
+
 PYBIND11_MODULE(_mvk, m) {
   m.doc() = "mivod hand-written gfx950 (CDNA4) kernels";
   m.attr("CHUNK") = kChunk;
   m.attr("MAX_TENSORS_PER_LAUNCH") = kMvMaxTensors;
+  m.def("tensor_from_ptr", &tensor_from_ptr, "tensor view of mivod-owned device memory");
   m.def("mt_copy", &mt_copy, "multi-tensor pack/unpack with fused cast+scale");
   m.def("flat_cast", &flat_cast, "flat cast + scale (compress/decompress)");
+  m.def("nonfinite_scan", &nonfinite_scan, "flag |= any non-finite element (read-only)");
   m.def("sgd_step", &sgd_step, "fused flat SGD(+momentum, nesterov) step");
   m.def("adam_step", &adam_step, "fused flat Adam/AdamW step");
   m.def("adadelta_step", &adadelta_step, "fused flat Adadelta step");
@@ -1519,7 +1544,8 @@ PYBIND11_MODULE(_mvk, m) {
         "{dx, dgamma, dbeta}: maxpool(3,2,1) backward fused with its producer BN+ReLU backward");
   m.def("stem_wgrad", &stem_wgrad, "ResNet stem conv weight gradient on MFMA (mv_stem.hip)");
   m.def("stem_fwd", &stem_fwd,
-        "{z, [P, 2, 64] partials}: ResNet 7x7/2 stem conv on MFMA with BN statistics (mv_stem.hip)");
+        "{z, [P, 2, 64] partials}: ResNet 7x7/2 stem conv on MFMA with BN statistics (mv_stem.hip)",
+        py::arg("x"), py::arg("w"), py::arg("shift") = py::none(), py::arg("grid") = 0);
   m.def("fold_coeffs", &fold_coeffs,
         "{co [5, cout], xsum [cin]}: the BN fold's per-channel coefficients (mv_fold.hip)");
   m.def("fold_products", &fold_products,

@@ -69,14 +69,21 @@ __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
   *reinterpret_cast<f32x4*>(p) = a;
   *reinterpret_cast<f32x4*>(p + 4) = b;
 }
-// Packed RNE f32x2 -> bf16x2 on gfx950 (lo <- a, hi <- b).  Written as inline
-// asm: ROCm 7.2 clang mis-lowers __builtin_convertvector(f32x2 -> bf16x2) inside
-// unrolled loops (it converted only the even elements: caught by
-// tests/test_kernels_gpu.py::test_pack_unpack_cast_scale).
+// Packed RNE f32x2 -> bf16x2 on gfx950 (lo <- a, hi <- b): one v_cvt_pk_bf16_f32,
+// selected by the compiler from a two-element build of scalar casts.
+//  * NOT __builtin_convertvector(f32x2 -> bf16x2): ROCm 7.2 clang mis-lowers it
+//    inside unrolled loops (only the even elements converted: caught by
+//    tests/test_kernels_gpu.py::test_pack_unpack_cast_scale).
+//  * NOT inline asm (round 1-2): the compiler's hazard recognizer cannot see into
+//    inline asm, so where MFMA accumulators live in VGPRs the asm read them 0-6
+//    wait states after the MFMA wrote them (CDNA needs 11 for 16x16x32; the
+//    hardware does not interlock) and got stale values — the NaN of
+//    stem_fwd_kernel at __launch_bounds__(256, 2) (round 3 root cause;
+//    scripts/check_mfma_asm_hazards.py checks every kernel for this).
 __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-  uint32_t r;
-  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 __device__ __forceinline__ void store8(__bf16* p, const float (&v)[8]) {

@@ -26,6 +26,8 @@ struct ChunkTable {
 
 void mv_launch_mt_copy(const MtArgs& a, int tensor_dtype, void* flat, int flat_dtype, bool to_flat,
                        float scale, int* found_nonfinite, hipStream_t st);
+// flag |= any(!isfinite(x)) (read-only)
+void mv_launch_nonfinite_scan(const void* x, int dtype, int64_t n, int* flag, hipStream_t st);
 void mv_launch_flat_cast(const void* src, int sd, void* dst, int dd, int64_t n, float scale,
                          int* found_nonfinite, hipStream_t st);
 void mv_launch_sgd(const void* g, int gd, float* w, float* mom, void* model, int md, int64_t n,

@@ -151,6 +151,46 @@ void mv_launch_flat_cast(const void* src, int sd, void* dst, int dd, int64_t n, 
 }
 
 // -------------------------------------------------------------------------
+// Overflow guard: read-only non-finite scan of a REDUCED bucket.  A non-finite
+// contribution of any rank (or an overflow inside the reduction) propagates
+// into the reduced sum, and every rank holds the same reduced bits, so every
+// rank sets the same flag without another collective.
+// -------------------------------------------------------------------------
+namespace mv {
+template <typename T>
+__global__ __launch_bounds__(kBlock) void nonfinite_scan_kernel(const T* __restrict__ x, int64_t n,
+                                                                 int* __restrict__ flag) {
+  const int64_t begin = (int64_t)blockIdx.x * kChunk;
+  const int64_t cnt = (n - begin < kChunk) ? (n - begin) : kChunk;
+  const T* s = x + begin;
+  bool bad = false;
+  if (aligned16(s)) {
+    const int64_t nv = cnt / kVec;
+    for (int64_t i = threadIdx.x; i < nv; i += kBlock) {
+      float v[8];
+      load8(s + i * kVec, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bad |= !__builtin_isfinite(v[j]);
+    }
+    for (int64_t i = nv * kVec + threadIdx.x; i < cnt; i += kBlock) bad |= !__builtin_isfinite(ld1(s + i));
+  } else {
+    for (int64_t i = threadIdx.x; i < cnt; i += kBlock) bad |= !__builtin_isfinite(ld1(s + i));
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+}  // namespace mv
+
+void mv_launch_nonfinite_scan(const void* x, int dt, int64_t n, int* flag, hipStream_t st) {
+  const int nb = (int)((n + kChunk - 1) / kChunk);
+  if (nb <= 0) return;
+  switch (dt) {
+    case F32: hipLaunchKernelGGL((nonfinite_scan_kernel<float>), dim3(nb), dim3(kBlock), 0, st, (const float*)x, n, flag); break;
+    case BF16: hipLaunchKernelGGL((nonfinite_scan_kernel<__bf16>), dim3(nb), dim3(kBlock), 0, st, (const __bf16*)x, n, flag); break;
+    case F16: hipLaunchKernelGGL((nonfinite_scan_kernel<_Float16>), dim3(nb), dim3(kBlock), 0, st, (const _Float16*)x, n, flag); break;
+  }
+}
+
+// -------------------------------------------------------------------------
 // K6: fused optimizers on flat buckets.
 // grad (TG: the wire / bucket dtype), fp32 master + fp32 state, and an optional
 // low-precision model copy (TP) written in the same pass.  Arena segments are

@@ -7,8 +7,9 @@
 int mv_stem_partials(int N);
 // z [N, 112, 112, 64] = conv7x7/2/pad3(x [N, 224, 224, 4], w [64, 7, 7, 4] (OHWC)), bf16
 // NHWC; partial [P][2][64] = per-channel (sum, sum^2) of bf16(z) - shift (shift may be null)
+// grid > 0 overrides the occupancy-sized grid (tests): partial then has `grid` rows
 void mv_stem_fwd(const void* x, const void* w, void* z, const float* shift, float* partial, int N,
-                 hipStream_t st);
+                 hipStream_t st, int grid = 0);
 // dw [64, 7, 7, 4] (OHWC bf16) = the stem conv's weight gradient from x [N, 224, 224, 4] and
 // dz [N, 112, 112, 64]; work: fp32 [mv_stem_wgrad_blocks(N) * 64 * 224]
 int mv_stem_wgrad_blocks(int N);

@@ -43,10 +43,13 @@ __device__ __forceinline__ f32x4v mfma(const bf16x8& a, const bf16x8& b, const f
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// NOTE (round 2): __launch_bounds__(256, 2) compiles this kernel to 236 VGPRs with the MFMA
-// accumulators in VGPRs (2 waves/SIMD, 1.21 vs 1.53 ms) but produced wrong outputs (NaN)
-// in test_stem_kernel_matches_fp32 on gfx950 — not understood yet; kept at 1 wave/SIMD.
-__global__ __launch_bounds__(256) void stem_fwd_kernel(const __bf16* __restrict__ x,
+// 2 waves/SIMD: 236 VGPRs with the MFMA accumulators in VGPRs (1.21 vs 1.53 ms at 1 wave).
+// Round 2 saw NaN at this bound: the epilogue's bf16 conversion was then inline asm, which
+// the compiler's hazard recognizer cannot see into, so it read the VGPR accumulators 0-6
+// wait states after the MFMA wrote them (11 needed; no hardware interlock) — fixed in
+// mv_common.h's cvt_pk_bf16 (compiler-selected now), checked by
+// scripts/check_mfma_asm_hazards.py; tests/test_conv_gpu.py runs every grid size.
+__global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const __bf16* __restrict__ x,
                                                        const __bf16* __restrict__ w,
                                                        __bf16* __restrict__ z,
                                                        const float* __restrict__ shift,
@@ -194,8 +197,8 @@ int mv_stem_partials(int N) {
 }
 
 void mv_stem_fwd(const void* x, const void* w, void* z, const float* shift, float* partial, int N,
-                 hipStream_t st) {
-  const int grid = mv_stem_partials(N);
+                 hipStream_t st, int grid) {
+  if (grid <= 0) grid = mv_stem_partials(N);
   hipLaunchKernelGGL(mv::stem::stem_fwd_kernel, dim3(grid), dim3(256), 0, st, (const __bf16*)x,
                      (const __bf16*)w, (__bf16*)z, shift, partial, N);
 }

@@ -202,7 +202,7 @@ def init(comm=None, process_sets=None):
                 from ..parallel.transport import RcclTransport
                 _state.gpu = RcclTransport.create(
                     0, 1, _state.device,
-                    timeout_s=float(os.environ.get("MIVOD_RCCL_TIMEOUT_S", "0") or 0))
+                    timeout_s=rccl_timeout_s(cfg))
                 _state.backend = "rccl"
         ORDER.reset(enabled=_state.gpu is not None and _state.size > 1)
         _state.initialized = True
@@ -223,7 +223,7 @@ def _make_gpu_plane(transport: str, world_backend: str, cfg) -> None:
     from ..parallel.transport import PgTransport, RcclTransport
     if transport == "rccl":
         store = dist.distributed_c10d._get_default_store()
-        timeout = float(os.environ.get("MIVOD_RCCL_TIMEOUT_S", cfg.stall_shutdown_time_s or 0.0))
+        timeout = rccl_timeout_s(cfg)
         ctas = int(os.environ.get("MIVOD_RCCL_CTAS", "0") or 0)
 
         def make(c: int, tag: str = "") -> "RcclTransport":
@@ -274,16 +274,30 @@ def _make_gpu_plane(transport: str, world_backend: str, cfg) -> None:
                 _state.gpu_cross = PgTransport(g, staged=staged, name=_state.gpu.name)
 
 
+def rccl_timeout_s(cfg=None) -> float:
+    """The RCCL watchdog timeout: ``MIVOD_RCCL_TIMEOUT_S``, else horovod's
+    ``HOROVOD_STALL_SHUTDOWN_TIME_SECONDS`` (0 = no timeout, horovod's default;
+    bench.py sets both for multi-rank runs)."""
+    cfg = cfg or _state.config or Config.from_env()
+    v = os.environ.get("MIVOD_RCCL_TIMEOUT_S", "")
+    return float(v) if v not in ("", None) else float(cfg.stall_shutdown_time_s or 0.0)
+
+
 def _make_mesh() -> None:
-    """MIVOD_MESH_MAX_MB > 0 and every rank on this node: the xGMI mesh one-shot
-    allreduce serves buckets up to that size (csrc/comm/mesh.hip)."""
+    """MIVOD_MESH_MAX_MB > 0 and every rank on this node: the xGMI mesh allreduce
+    serves buckets up to that size (csrc/comm/mesh.hip) — one-shot up to
+    MIVOD_MESH_ONESHOT_KB (default 1024), two-shot above."""
     mb = float(os.environ.get("MIVOD_MESH_MAX_MB", "0") or 0)
     if mb <= 0 or _state.local_size != _state.size or _state.size > 16:
         return
     from ..parallel.transport import MeshTransport
     store = dist.distributed_c10d._get_default_store()
+    tmo = float(os.environ.get("MIVOD_MESH_TIMEOUT_S", "") or rccl_timeout_s() or 30.0)
+    one_kb = float(os.environ.get("MIVOD_MESH_ONESHOT_KB", "1024") or 1024)
     _state.mesh = MeshTransport(_state.rank, _state.size, _state.device, int(mb * 2 ** 20), store,
-                                key=f"mivod/mesh/{_state.init_count}")
+                                key=f"mivod/mesh/{_state.init_count}", timeout_s=tmo,
+                                exit_on_timeout=os.environ.get("MIVOD_MESH_TIMEOUT_EXIT", "1")
+                                != "0", oneshot_max_bytes=int(one_kb * 1024))
 
 
 def _make_hierarchy_groups():

@@ -8,7 +8,7 @@ are also the fp32 references the numerics tests compare the kernels against.
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional, Sequence
 
 import torch
@@ -113,6 +113,16 @@ def flat_cast(src: torch.Tensor, dst: torch.Tensor, scale: float = 1.0,
     dst.copy_(v)
 
 
+def nonfinite_scan(x: torch.Tensor, flag: torch.Tensor) -> None:
+    """flag |= any non-finite element of ``x`` (read-only; the overflow guard's
+    per-bucket check of the REDUCED gradient)."""
+    if _on_gpu(x):
+        native().nonfinite_scan(x, flag)
+        return
+    if not bool(torch.isfinite(x.float()).all()):
+        flag.fill_(1)
+
+
 # ---------------------------------------------------------------------------
 # K6 fused optimizers (flat)
 # ---------------------------------------------------------------------------
@@ -201,6 +211,9 @@ class ChunkTable:
     seg_nc: torch.Tensor
     seg_offsets: list
     total: int
+    # derived tables (e.g. Adasum's per-level clipped ranges), owned by this
+    # table so they can never outlive it or be served to another table
+    derived: dict = field(default_factory=dict, repr=False, compare=False)
 
     @property
     def nchunks(self) -> int:
@@ -349,3 +362,10 @@ def adasum_fcombine(f: torch.Tensor, r: torch.Tensor, table: ChunkTable, dots: t
         cf, cr = (cb, ca) if swap else (ca, cb)
         x = f[off:off + n]
         x.copy_(cf * x + cr * r[off:off + n].float())
+
+
+def tensor_from_ptr(ptr: int, numel: int, dtype: torch.dtype, device) -> torch.Tensor:
+    """A 1-D tensor over device memory mivod owns elsewhere (the xGMI mesh's
+    IPC staging slot) — no copy; the owner must outlive the view."""
+    dev = torch.device(device)
+    return native().tensor_from_ptr(int(ptr), int(numel), dtype, dev.index or 0)

@@ -14,9 +14,9 @@ bandwidth-optimal **vector-halving / distance-doubling** schedule:
   each sends the half it gives away (wire dtype) and receives the partner's
   copy of the half it keeps.  The per-tensor Gram terms (a.b, |a|^2, |b|^2) of
   that level are partial sums over the kept piece, so they are summed over the
-  2^(i+1) ranks that jointly hold the two vectors being merged (one small fp32
-  allreduce; each rank writes its partial into its group's slot).  Then each
-  rank merges its kept piece.
+  2^(i+1) ranks that jointly hold the two vectors being merged (recursive
+  doubling inside that group: i+1 exchanges of nseg*3 fp32 — no world-wide
+  traffic).  Then each rank merges its kept piece.
 * allgather phase: the levels in reverse, each rank swaps its finished piece
   with its partner until everyone holds the whole result.
 
@@ -38,7 +38,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Dict, Tuple
+from typing import Dict
 
 import torch
 
@@ -52,7 +52,6 @@ ALIGN = 64
 LAST = {"exchange_bytes": 0, "dot_bytes": 0, "levels": 0}
 
 _WS: Dict[tuple, torch.Tensor] = {}
-_TABLES: Dict[tuple, K.ChunkTable] = {}
 
 
 def _is_pow2(n: int) -> bool:
@@ -78,9 +77,13 @@ def _scratch(name: str, numel: int, dtype: torch.dtype, device) -> torch.Tensor:
 
 
 def _clipped(table: K.ChunkTable, lo: int, hi: int, device) -> K.ChunkTable:
-    """Chunk table of ``table``'s segments clipped to [lo, hi) (segment ids kept)."""
-    key = (id(table), table.total, lo, hi, str(device))
-    t = _TABLES.get(key)
+    """Chunk table of ``table``'s segments clipped to [lo, hi) (segment ids kept).
+
+    Cached on ``table`` itself (``ChunkTable.derived``): the clipped tables live
+    and die with their parent, so a new table that happens to reuse a freed
+    one's address can never be served the old segment boundaries."""
+    key = ("adasum-clip", lo, hi, str(device))
+    t = table.derived.get(key)
     if t is None:
         sizes, offs = [], []
         for off, n in zip(table.seg_offsets, table.seg_sizes):
@@ -88,8 +91,26 @@ def _clipped(table: K.ChunkTable, lo: int, hi: int, device) -> K.ChunkTable:
             sizes.append(max(0, b - a))
             offs.append(a if b > a else lo)
         t = K.make_chunk_table(sizes, device, offs)
-        _TABLES[key] = t
+        table.derived[key] = t
     return t
+
+
+def _group_sum_(part: torch.Tensor, tr, rank: int, level: int) -> int:
+    """Sum ``part`` (a rank's [nseg, 3] Gram partial) over the 2^(level+1) ranks
+    that share ``rank >> (level+1)`` — the ranks jointly holding the two vectors
+    merged at this level — by recursive doubling inside that group (level+1
+    send/recv exchanges of nseg*3 floats).  Traffic is independent of the world
+    size (the old scheme allreduced a zero-padded [world/2^(level+1), nseg, 3]
+    buffer over the whole world).  IEEE addition is commutative, so both sides
+    of every exchange compute the same bits: the group ends bitwise identical.
+    Returns the bytes this rank sent."""
+    recv = torch.empty_like(part)
+    sent = 0
+    for j in range(level + 1):
+        tr.sendrecv(part, recv, rank ^ (1 << j))
+        part.add_(recv)
+        sent += part.numel() * 4
+    return sent
 
 
 def adasum_vhdd_(buf: torch.Tensor, table: K.ChunkTable, tr) -> torch.Tensor:
@@ -128,12 +149,10 @@ def adasum_vhdd_(buf: torch.Tensor, table: K.ChunkTable, tr) -> torch.Tensor:
         part = K.seg_dot3(f, rw, tk)                   # (f.r, |f|^2, |r|^2)
         if not lower:
             part = part[:, [0, 2, 1]]                   # -> (a.b, |a|^2, |b|^2)
-        groups = n_ranks >> (i + 1)
-        gbuf = torch.zeros(groups, nseg, 3, dtype=torch.float32, device=dev)
-        gbuf[rank >> (i + 1)] = part
-        tr.allreduce_(gbuf, T.SUM)
-        dots_b += gbuf.numel() * 4
-        K.adasum_fcombine(f, rw, tk, gbuf[rank >> (i + 1)], swap=not lower)
+        part = part.contiguous()
+        assert part.shape == (nseg, 3)
+        dots_b += _group_sum_(part, tr, rank, i)
+        K.adasum_fcombine(f, rw, tk, part, swap=not lower)
         lo, hi = klo, khi
     if hi > lo:
         K.flat_cast(f[lo:hi], buf[lo:hi])
@@ -220,5 +239,5 @@ def adasum_reference(vectors, table: K.ChunkTable) -> torch.Tensor:
     return vs[0]
 
 
-def _peek_cache() -> Tuple[int, int]:
-    return len(_WS), len(_TABLES)
+def _peek_cache() -> int:
+    return len(_WS)

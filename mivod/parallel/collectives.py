@@ -92,6 +92,7 @@ def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
                   and st.mesh.accepts(flat, _TOP[op])):
                 st.mesh.allreduce_(flat, _TOP[op], prescale)     # small bucket: one xGMI hop
             elif (st.config is not None and st.config.hierarchical_allreduce and group is None
+                  and _hier_ok(flat, op, prescale)
                   and st.gpu_local is not None and st.gpu_cross is not None):
                 _hierarchical_gpu_(flat, op, prescale)
             else:
@@ -107,8 +108,9 @@ def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
     if op == Adasum:
         from .adasum import adasum_allreduce_
         return adasum_allreduce_(t, adasum_table)
-    if (st.config is not None and st.config.hierarchical_allreduce and st.local_pg is not None
-            and st.cross_pg is not None and group is None and not engine):
+    if (st.config is not None and st.config.hierarchical_allreduce and op in (Average, Sum)
+            and st.local_pg is not None and st.cross_pg is not None and group is None
+            and not engine):
         return _hierarchical_cpu_(t, op)
     ring = _ring(t, group, engine)
     if ring is not None and op in (Average, Sum):
@@ -130,25 +132,46 @@ def allreduce_(t: torch.Tensor, op: int = Sum, group=None, engine: bool = False,
     return t
 
 
+def _hier_ok(t: torch.Tensor, op: int, prescale: float) -> bool:
+    """Ops the two-level schedule computes exactly: Sum / Average (integer
+    tensors only as an unscaled Sum — the scale is a floating-point pass)."""
+    if op not in (Average, Sum):
+        return False
+    return t.dtype.is_floating_point or (op == Sum and prescale == 1.0)
+
+
 def _hierarchical_gpu_(flat: torch.Tensor, op: int, prescale: float) -> None:
-    """HOROVOD_HIERARCHICAL_ALLREDUCE on GPU: intra-node reduce-scatter (xGMI),
-    cross-node allreduce of each 1/local_size shard (the network carries 1/L of
-    the bytes), intra-node allgather — three RCCL calls on ncclCommSplit comms."""
+    """HOROVOD_HIERARCHICAL_ALLREDUCE on GPU (Sum / Average only): intra-node
+    reduce-scatter (xGMI), cross-node allreduce of each 1/local_size shard (the
+    network carries 1/L of the bytes), intra-node allgather — RCCL calls on
+    ncclCommSplit comms, all IN PLACE on ``flat`` (no padded copy).  The average
+    and ``prescale`` are one scale of the SHARD (1/L of the buffer) by mivod's
+    flat-cast kernel after the cross-node sum (the sum is linear), not a pass
+    over the whole buffer.  (Not RCCL PreMulSum: RCCL 2.26 leaves the last
+    element of an odd-length 1-rank PreMulSum unscaled — tests/
+    test_multirank_gpu.py::test_gpu_rccl_communicator_world1 caught it.)  The
+    ``n % L`` tail elements that do not split evenly take one small allreduce on
+    the world communicator.  Max / Min never come here (they run flat)."""
+    from ..ops import kernels as K
     st = basics.state()
     L = st.gpu_local.size
-    if prescale != 1.0:
-        flat.mul_(prescale)
+    scale = float(prescale) / (st.size if op == Average else 1)
     n = flat.numel()
-    pad = (-n) % L
-    work = flat if pad == 0 else torch.cat([flat, flat.new_zeros(pad)])
-    shard = torch.empty(work.numel() // L, dtype=flat.dtype, device=flat.device)
-    st.gpu_local.reduce_scatter(shard, work, T.SUM)
-    st.gpu_cross.allreduce_(shard, T.SUM)
-    st.gpu_local.allgather_into(work, shard)
-    if pad:
-        flat.copy_(work[:n])
-    if op == Average:
-        flat.div_(st.size)
+    m = n - n % L
+    if m:
+        body = flat[:m]
+        c = m // L
+        shard = body[st.gpu_local.rank * c:(st.gpu_local.rank + 1) * c]
+        st.gpu_local.reduce_scatter(shard, body, T.SUM)       # in place (recvbuf in sendbuf)
+        st.gpu_cross.allreduce_(shard, T.SUM)
+        if scale != 1.0:
+            K.flat_cast(shard, shard, scale)
+        st.gpu_local.allgather_into(body, shard)              # in place (sendbuf in recvbuf)
+    if m < n:
+        tail = flat[m:]
+        st.gpu.allreduce_(tail, T.SUM)
+        if scale != 1.0:
+            K.flat_cast(tail, tail, scale)
 
 
 def _hierarchical_cpu_(t: torch.Tensor, op: int = Sum) -> torch.Tensor:
@@ -169,7 +192,10 @@ def _hierarchical_cpu_(t: torch.Tensor, op: int = Sum) -> torch.Tensor:
 
 def hierarchical_allreduce_(t: torch.Tensor, op: int = Sum) -> torch.Tensor:
     st = basics.state()
-    if t.is_cuda and st.gpu_local is not None and st.gpu_cross is not None:
+    if op not in (Average, Sum):
+        return allreduce_(t, op)          # Max / Min: flat (see _hierarchical_gpu_)
+    if t.is_cuda and st.gpu_local is not None and st.gpu_cross is not None \
+            and _hier_ok(t, op, 1.0):
         with ORDER.issue():
             flat = _flat(t)
             _hierarchical_gpu_(flat, op, 1.0)

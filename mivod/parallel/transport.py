@@ -76,6 +76,10 @@ class RcclTransport:
         return cls(m.Comm(bytes(uid), rank, size, device.index, float(timeout_s),
                           bool(exit_on_abort), int(min_ctas), int(max_ctas)))
 
+    def count(self) -> int:
+        """ncclCommCount — the ranks RCCL itself sees (bench self-diagnosis)."""
+        return int(self.comm.count())
+
     @property
     def ctas(self):
         """(minCTAs, maxCTAs) this communicator was created with (0: RCCL default)."""
@@ -306,20 +310,32 @@ class PgTransport:
 
 
 class MeshTransport:
-    """xGMI mesh one-shot allreduce (``mivod._mvcomm.Mesh``, csrc/comm/mesh.hip) for
-    small buckets: every rank reads every peer's HIP-IPC-mapped staging copy and
-    reduces locally in fixed rank order (bit-identical on all ranks).  Used for
-    Sum/Average of fp32/bf16/fp16 buffers of at most ``MIVOD_MESH_MAX_MB``; all
-    ranks must share one node.  Parity: SURVEY.md §2.5 K7."""
+    """xGMI mesh allreduce (``mivod._mvcomm.Mesh``, csrc/comm/mesh.hip) for small
+    and medium buckets: one-shot (every rank reads every peer's HIP-IPC-mapped
+    staging copy and reduces locally) up to ``MIVOD_MESH_ONESHOT_KB``, two-shot
+    (mesh reduce-scatter into IPC result buffers + all-gather from them) above,
+    both in fixed rank order (bit-identical on all ranks).  Used for Sum/Average
+    of fp32/bf16/fp16 buffers of at most ``MIVOD_MESH_MAX_MB``; all ranks must
+    share one node.  A producer can write straight into the next call's staging
+    slot (``stage_view``) — the bucket pack kernel does — saving the copy.
+
+    A peer that does not arrive within ``timeout_s`` (``MIVOD_MESH_TIMEOUT_S``,
+    default the RCCL watchdog timeout or 30 s) poisons the output with NaN, and
+    the native watcher thread ends the process with a diagnosis — a rank never
+    trains on its local gradient.  Parity: SURVEY.md §2.5 K7."""
 
     name = "mesh"
     _CODES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
     def __init__(self, rank: int, size: int, device: torch.device, capacity_bytes: int, store,
-                 key: str):
+                 key: str, timeout_s: float = 30.0, exit_on_timeout: bool = True,
+                 oneshot_max_bytes: int = 2 ** 20):
         m = _mvcomm()
         self.rank, self.size = rank, size
-        self.mesh = m.Mesh(rank, size, device.index, int(capacity_bytes))
+        self.device = device
+        self.mesh = m.Mesh(rank, size, device.index, int(capacity_bytes), float(timeout_s),
+                           bool(exit_on_timeout))
+        self.mesh.oneshot_max_bytes = int(oneshot_max_bytes)
         store.set(f"{key}/{rank}", self.mesh.handles())
         hs = [bytes(store.get(f"{key}/{r}")) for r in range(size)]
         self.mesh.open(hs)
@@ -330,17 +346,34 @@ class MeshTransport:
                 and t.numel() * t.element_size() <= self.capacity
                 and t.data_ptr() % 16 == 0)
 
+    def stage_view(self, numel: int, dtype: torch.dtype) -> Optional[torch.Tensor]:
+        """A tensor over the staging slot the NEXT allreduce reads (None if it
+        does not fit): write the bucket there, then ``allreduce_into``."""
+        if dtype not in self._CODES or numel * torch.empty((), dtype=dtype).element_size() \
+                > self.capacity:
+            return None
+        from ..ops import kernels as K
+        return K.tensor_from_ptr(self.mesh.stage_ptr(), numel, dtype, self.device)
+
     def allreduce_(self, t: torch.Tensor, op: str = SUM, prescale: float = 1.0) -> torch.Tensor:
+        return self.allreduce_into(t, t, op, prescale)
+
+    def allreduce_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = SUM,
+                       prescale: float = 1.0, algo: int = 0) -> torch.Tensor:
+        """out = reduce(inp) over the mesh; ``inp`` may be a ``stage_view``."""
+        assert out.numel() == inp.numel() and out.dtype == inp.dtype
         scale = float(prescale) * (1.0 / self.size if op == AVG else 1.0)
-        self.mesh.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), self._CODES[t.dtype], scale,
-                            _stream())
-        return t
+        self.mesh.allreduce(inp.data_ptr(), out.data_ptr(), out.numel(), self._CODES[out.dtype],
+                            scale, _stream(), algo)
+        return out
 
     def status(self) -> int:
         return self.mesh.status()
 
     def stats(self) -> dict:
-        return {"mesh_calls": self.mesh.calls, "mesh_bytes": self.mesh.bytes}
+        return {"mesh_calls": self.mesh.calls, "mesh_bytes": self.mesh.bytes,
+                "mesh_two_shot_calls": self.mesh.two_shot_calls,
+                "mesh_copies_saved": self.mesh.copies_saved}
 
     def close(self):
         self.mesh.close()

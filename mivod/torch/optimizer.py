@@ -26,11 +26,17 @@ MI355X design (not a translation of horovod's per-tensor async ops):
   whole update overlaps the remaining backward; ``step()`` is then only a
   stream wait.  Plain torch optimizers get zero-copy gradient views into the
   reduced bucket instead.
-* **Overflow guard** (default with fp16 wire compression): the pack kernel
-  flags non-finite values (bf16 gradients above the fp16 range included), one
-  4-byte MAX-allreduce makes the flag identical on every rank, and the fused
-  update kernels read it on the device and skip the step — every rank skips
-  identically, with no host sync.  ``grad_scale="dynamic"`` additionally
+* **Overflow guard** (default with fp16 wire compression): after each bucket's
+  collective a read-only scan kernel checks the REDUCED bucket — a non-finite
+  contribution of any rank (bf16 gradients above the fp16 range included) or an
+  fp16 overflow inside the reduction is non-finite there, with the same bits on
+  every rank, so every rank sets the same device flag with no extra collective
+  and no host sync.  Default ``MIVOD_GUARD_MODE=bucket``: the bucket's fused
+  update runs immediately (overlapped with the rest of backward) and skips
+  itself when its bucket is non-finite — the other buckets of that step are
+  applied; an arena whose every bucket was skipped does not count the step.
+  ``MIVOD_GUARD_MODE=step``: one flag per step and every update deferred to
+  after the last bucket (horovod / AMP whole-step skip, not overlapped).  ``grad_scale="dynamic"`` additionally
   scales the wire by s (halved after an overflow, doubled back after
   ``MIVOD_GUARD_GROWTH_STEPS`` clean steps, capped at 1) and folds 1/s into the
   update.
@@ -51,6 +57,7 @@ from ..ops import kernels as K
 from ..ops.compression import Compression
 from ..optim.fused import Arena, FusedOptimizer, _align
 from ..parallel import collectives as C
+from ..parallel.order import ORDER
 from ..utils import markers as MK
 from ..utils import timeline as TL
 
@@ -269,11 +276,21 @@ class _DistributedOptimizerMixin:
         self._mvd_gs = float(grad_scale) if isinstance(grad_scale, (int, float)) else 1.0
         self._mvd_gs_growth = int(os.environ.get("MIVOD_GUARD_GROWTH_STEPS", "200"))
         self._mvd_gs_good = 0
-        self._mvd_flag = None             # device int32 non-finite flag of the step
-        self._mvd_flag_host = None        # pinned copy + event of the previous step's flag
+        # "bucket" (default): each reduced bucket is scanned and its fused update
+        # runs right away, skipped on every rank when that bucket is non-finite
+        # (overlapped with backward); "step": one flag for the whole step, every
+        # update deferred until the last bucket is reduced (horovod / AMP
+        # whole-step semantics, not overlapped)
+        self._mvd_guard_mode = os.environ.get("MIVOD_GUARD_MODE", "bucket")
+        if self._mvd_guard_mode not in ("bucket", "step"):
+            raise ValueError("MIVOD_GUARD_MODE must be 'bucket' or 'step'")
+        self._mvd_flag = None             # device int32 non-finite flags of the step
+        self._mvd_flag_host = None        # pinned copy + event of the previous step's flags
         self._mvd_flag_ev = None
+        self._mvd_flag_plan = None        # the bucket plan those flags index
         self._mvd_skipped = 0
         self._mvd_rec = None
+        self._mvd_comm_log = None         # time_comm(): [(bucket, bytes, ev0, ev1)]
         self._mvd_autotune = None
         if cfg.autotune and bucket_mb is None and first_bucket_mb is None:
             from ..parallel.autotune import BucketAutotuner
@@ -295,7 +312,8 @@ class _DistributedOptimizerMixin:
         import hashlib
         h = hashlib.blake2b(digest_size=8)
         h.update(repr((C.op_name(self._mvd_op), self._mvd_compression.__name__,
-                       self._mvd_bpps, self._mvd_guard, self._mvd_gs)).encode())
+                       self._mvd_bpps, self._mvd_guard, self._mvd_gs,
+                       self._mvd_guard_mode if self._mvd_guard else "")).encode())
         for b in self._mvd_buckets:
             h.update(repr((str(b.arena.grad.dtype), b.hi - b.lo,
                            [(self._mvd_names[id(p)], tuple(p.shape)) for p in b.params])).encode())
@@ -329,39 +347,81 @@ class _DistributedOptimizerMixin:
             self._mvd_launch(bs[self._mvd_next])
             self._mvd_next += 1
 
-    def _mvd_guard_begin(self, device):
-        """Step start (guard on): consume the previous step's flag — read at the
-        same step on every rank (the wait is for a flag allreduced at the end of
-        the previous step, long done by now), adjust the dynamic scale, reset."""
-        if self._mvd_flag_ev is not None:
-            self._mvd_flag_ev.synchronize()
-            if int(self._mvd_flag_host[0]) != 0:
-                self._mvd_skipped += 1
-                if self._mvd_fused:
-                    for a in self._mvd_arenas:
-                        a.step = max(a.step - 1, 0)   # the skipped update did not count
-                msg = (f"mivod: non-finite gradients on the fp16 wire (or in the gradients) — "
-                       f"optimizer step {self._mvd_steps} skipped on every rank")
-                if self._mvd_dynamic:
-                    self._mvd_gs = max(self._mvd_gs * 0.5, 2.0 ** -24)
-                    msg += f"; wire scale -> {self._mvd_gs:g}"
-                    self._mvd_gs_good = 0
-                _log.warning(msg)
-                warnings.warn(msg)
-            elif self._mvd_dynamic:
-                self._mvd_gs_good += 1
-                if self._mvd_gs_good >= self._mvd_gs_growth and self._mvd_gs < 1.0:
-                    self._mvd_gs = min(self._mvd_gs * 2.0, 1.0)
-                    self._mvd_gs_good = 0
-            self._mvd_flag_ev = None
-        if self._mvd_flag is None:
-            self._mvd_flag = torch.zeros(1, dtype=torch.int32, device=device)
-            if device.type == "cuda":
-                self._mvd_flag_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+    def _mvd_resolve_flags(self):
+        """Consume the previous step's overflow flags (host wait on an event
+        recorded after that step's last fused update — long done by the time the
+        next step starts): skipped-step count, optimizer step counters, dynamic
+        wire scale.  Every rank reads the same flags (they come from the reduced
+        buckets), so every rank takes the same decisions."""
+        if self._mvd_flag_ev is None:
+            return
+        self._mvd_flag_ev.synchronize()
+        flags = [int(v) for v in self._mvd_flag_host.tolist()]
+        plan = self._mvd_flag_plan or []
+        self._mvd_flag_ev = None
+        self._mvd_flag_plan = None
+        if any(flags):
+            self._mvd_skipped += 1
+            if self._mvd_guard_mode == "step":
+                skipped = list(plan)
+                what = f"optimizer step {self._mvd_steps} skipped on every rank"
             else:
-                self._mvd_flag_host = torch.zeros(1, dtype=torch.int32)
+                skipped = [b for b in plan if flags[b.index]]
+                what = (f"{len(skipped)} of {len(plan)} gradient buckets of optimizer step "
+                        f"{self._mvd_steps} skipped on every rank ("
+                        + ", ".join(b.name for b in skipped) + ")")
+            if self._mvd_fused:
+                for a in self._mvd_arenas:
+                    mine = [b for b in plan if b.arena is a]
+                    if mine and all(b in skipped for b in mine):
+                        a.step = max(a.step - 1, 0)   # no update of this arena counted
+            msg = f"mivod: non-finite gradients on the fp16 wire (or in the gradients) — {what}"
+            if self._mvd_dynamic:
+                self._mvd_gs = max(self._mvd_gs * 0.5, 2.0 ** -24)
+                msg += f"; wire scale -> {self._mvd_gs:g}"
+                self._mvd_gs_good = 0
+            _log.warning(msg)
+            warnings.warn(msg)
+        elif self._mvd_dynamic:
+            self._mvd_gs_good += 1
+            if self._mvd_gs_good >= self._mvd_gs_growth and self._mvd_gs < 1.0:
+                self._mvd_gs = min(self._mvd_gs * 2.0, 1.0)
+                self._mvd_gs_good = 0
+
+    def _mvd_guard_begin(self, device):
+        """Step start (guard on): consume the previous step's flags, then reset."""
+        self._mvd_resolve_flags()
+        nf = len(self._mvd_buckets) if self._mvd_guard_mode == "bucket" else 1
+        if self._mvd_flag is None or self._mvd_flag.numel() != nf:
+            self._mvd_flag = torch.zeros(nf, dtype=torch.int32, device=device)
+            self._mvd_flag_host = torch.zeros(nf, dtype=torch.int32)
+            if device.type == "cuda":
+                self._mvd_flag_host = self._mvd_flag_host.pin_memory()
         else:
             self._mvd_flag.zero_()
+
+    def _mvd_bucket_flag(self, b: _Bucket):
+        """The device flag a bucket's scan sets and its fused update reads."""
+        if self._mvd_guard_mode == "bucket":
+            return self._mvd_flag[b.index:b.index + 1]
+        return self._mvd_flag[0:1]
+
+    def state_dict(self):
+        # a step skipped by the overflow guard must not be counted in the saved
+        # optimizer state (its flags are otherwise read at the next step's start)
+        if getattr(self, "_mvd_guard", False):
+            self._mvd_resolve_flags()
+        return super().state_dict()
+
+    def _mvd_mesh_for(self, flat: torch.Tensor, cuda: bool, inplace: bool):
+        """The xGMI mesh transport when this bucket rides it (pack straight into
+        the mesh's IPC staging slot), else None."""
+        st = basics.state()
+        mesh = st.mesh
+        if (mesh is None or not cuda or not self._mvd_comm or inplace
+                or self._mvd_op == C.Adasum):
+            return None
+        return mesh if mesh.accepts(flat, "sum") else None
 
     def _mvd_launch(self, b: _Bucket):
         a = b.arena
@@ -375,19 +435,19 @@ class _DistributedOptimizerMixin:
         size = self._mvd_size
         prescale = 1.0 / self._mvd_predivide if self._mvd_op == C.Average else 1.0
         prescale *= self._mvd_gs
-        flag = self._mvd_flag if self._mvd_guard else None
         rec = self._mvd_rec
         t_pack = rec.event() if rec is not None and a.grad.is_cuda else (
             rec.host() if rec is not None else None)
         groups: Dict[torch.dtype, tuple] = {}
-        scan_inplace = False
+        missing = []
+        inplace = False
         with torch.no_grad():
             for k, p in enumerate(b.params):
                 i = b.i0 + k
                 g = p.grad
                 lo = a.offsets[i]
                 if g is None:
-                    a.grad[lo:lo + p.numel()].zero_()
+                    missing.append((lo, p.numel()))
                     continue
                 if g.is_sparse:
                     g = g.to_dense()          # sparse_as_dense (embedding grads)
@@ -395,56 +455,78 @@ class _DistributedOptimizerMixin:
                         g.dtype == a.grad.dtype and g.stride() == p.stride():
                     if prescale != 1.0:
                         g.mul_(prescale)
-                    scan_inplace = flag is not None
+                    inplace = True
                     continue  # gradient already lives in its bucket slot (accumulated in place)
                 if g.stride() != p.stride() or not K.is_dense(g):
                     g = torch.empty_like(p, dtype=g.dtype).copy_(g)
                 ent = groups.setdefault(g.dtype, ([], []))
                 ent[0].append(g)
                 ent[1].append(lo)
-            with MK.range(f"mivod.pack.{b.name}"):
-                for dt, (gl, ol) in groups.items():
-                    K.pack(gl, a.grad, ol, scale=prescale, nonfinite=flag)
-                if scan_inplace:      # zero-copy grads are scanned in place
-                    seg = a.grad[b.lo:b.hi]
-                    K.flat_cast(seg, seg, 1.0, flag)
-            if self._mvd_fused:
-                for p in b.params:
-                    p.grad = None            # freed on the compute stream after the pack
         flat = a.grad[b.lo:b.hi]
         # inline (no comm-stream fork; launched from synchronize(), after backward) while
         # a single-rank step is captured into a HIP graph: ROCm runs a two-stream graph
         # DAG ~15 us/kernel slower than one chain (scripts/debug/graph_speed.py), and
         # with one rank there is no RCCL to overlap
         cuda = flat.is_cuda and self._mvd_stream is not None and not self._mvd_inline
-        t_packed = None
-        if rec is not None:
-            t_packed = rec.event() if flat.is_cuda else rec.host()
-            rec.add(b.name, "MEMCPY_IN_FUSION_BUFFER", t_pack, t_packed)
-        if cuda:
-            ev = torch.cuda.Event()
-            ev.record()
-            ctx = torch.cuda.stream(self._mvd_stream)
-        else:
-            ctx = contextlib.nullcontext()
-        with ctx:
+        mesh = self._mvd_mesh_for(flat, cuda, inplace)
+        # the mesh's staging slot is chosen by its call count, so pack + collective
+        # are ONE entry of the cross-rank issue order (no collective in between)
+        order = ORDER.issue() if mesh is not None else contextlib.nullcontext()
+        with order:
+            with torch.no_grad():
+                if mesh is not None:
+                    dst, base = mesh.stage_view(flat.numel(), flat.dtype), b.lo
+                else:
+                    dst, base = a.grad, 0
+                for lo, n in missing:
+                    dst[lo - base:lo - base + n].zero_()
+                with MK.range(f"mivod.pack.{b.name}"):
+                    for dt, (gl, ol) in groups.items():
+                        K.pack(gl, dst, [o - base for o in ol], scale=prescale)
+                if self._mvd_fused:
+                    for p in b.params:
+                        p.grad = None            # freed on the compute stream after the pack
+            t_packed = None
+            if rec is not None:
+                t_packed = rec.event() if flat.is_cuda else rec.host()
+                rec.add(b.name, "MEMCPY_IN_FUSION_BUFFER", t_pack, t_packed)
             if cuda:
-                self._mvd_stream.wait_event(ev)
-            if self._mvd_comm:
-                t0 = (rec.event() if cuda else rec.host()) if rec is not None else None
-                with MK.range(f"mivod.allreduce.{b.name}"):
-                    if self._mvd_op == C.Adasum:
-                        C.allreduce_(flat, C.Adasum, adasum_table=a.table(b.i0, b.i1))
-                    elif self._mvd_fused:
-                        C.allreduce_(flat, C.Sum)
-                    else:
-                        C.allreduce_(flat, C.Average if self._mvd_op == C.Average else C.Sum)
-                if rec is not None:
-                    phase = "ADASUM" if self._mvd_op == C.Adasum else (
-                        "NCCL_ALLREDUCE" if cuda else "RING_ALLREDUCE")
-                    rec.add(b.name, phase, t0, rec.event() if cuda else rec.host())
+                ev = torch.cuda.Event()
+                ev.record()
+                ctx = torch.cuda.stream(self._mvd_stream)
+            else:
+                ctx = contextlib.nullcontext()
+            with ctx:
+                if cuda:
+                    self._mvd_stream.wait_event(ev)
+                if self._mvd_comm:
+                    t0 = (rec.event() if cuda else rec.host()) if rec is not None else None
+                    c0 = self._mvd_comm_event() if cuda else None
+                    with MK.range(f"mivod.allreduce.{b.name}"):
+                        if mesh is not None:
+                            avg = self._mvd_op == C.Average and not self._mvd_fused
+                            mesh.allreduce_into(flat, dst, "avg" if avg else "sum")
+                        elif self._mvd_op == C.Adasum:
+                            C.allreduce_(flat, C.Adasum, adasum_table=a.table(b.i0, b.i1))
+                        elif self._mvd_fused:
+                            C.allreduce_(flat, C.Sum)
+                        else:
+                            C.allreduce_(flat, C.Average if self._mvd_op == C.Average else C.Sum)
+                    if c0 is not None:
+                        self._mvd_comm_log.append((b.name, b.nbytes, c0, self._mvd_comm_event()))
+                    if rec is not None:
+                        phase = "ADASUM" if self._mvd_op == C.Adasum else (
+                            "MESH_ALLREDUCE" if mesh is not None else (
+                                "NCCL_ALLREDUCE" if cuda else "RING_ALLREDUCE"))
+                        rec.add(b.name, phase, t0, rec.event() if cuda else rec.host())
+        with (torch.cuda.stream(self._mvd_stream) if cuda else contextlib.nullcontext()):
+            if self._mvd_guard:
+                # overflow guard: scan the REDUCED bucket (a non-finite contribution
+                # of any rank, or an fp16 overflow in the reduction, is non-finite
+                # here, identically on every rank — no extra collective)
+                K.nonfinite_scan(flat, self._mvd_bucket_flag(b))
             if self._mvd_fused:
-                if not self._mvd_guard:
+                if not self._mvd_guard or self._mvd_guard_mode == "bucket":
                     self._mvd_apply_bucket(b, cuda)
             else:
                 post = self._mvd_predivide if (self._mvd_op == C.Average and size > 1) else 1.0
@@ -461,6 +543,32 @@ class _DistributedOptimizerMixin:
                 self._mvd_done_event = ev2
         b.launched = True
 
+    # ------------------------------------------------------- comm timing
+    def _mvd_comm_event(self):
+        if self._mvd_comm_log is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def time_comm(self, enable: bool = True):
+        """Record a timing-event pair around every bucket collective (on the comm
+        stream) from now on — bench.py's measured per-bucket allreduce time and
+        bus bandwidth.  ``comm_timings()`` reads and clears them."""
+        self._mvd_comm_log = [] if enable else None
+
+    def comm_timings(self) -> List[tuple]:
+        """[(bucket name, payload bytes, ms)] of every collective recorded since
+        ``time_comm()`` / the last call (waits for them to finish)."""
+        log = self._mvd_comm_log or []
+        out = []
+        for name, nb, e0, e1 in log:
+            e1.synchronize()
+            out.append((name, nb, e0.elapsed_time(e1)))
+        if self._mvd_comm_log is not None:
+            self._mvd_comm_log = []
+        return out
+
     def _mvd_apply_bucket(self, b: _Bucket, cuda: bool):
         """The fused optimizer step of one reduced bucket (current stream)."""
         rec = self._mvd_rec
@@ -468,7 +576,7 @@ class _DistributedOptimizerMixin:
         if self._mvd_op == C.Average:
             gscale *= self._mvd_predivide / self._mvd_size
         t0 = (rec.event() if cuda else rec.host()) if rec is not None else None
-        self._mv_skip = self._mvd_flag if self._mvd_guard else None
+        self._mv_skip = self._mvd_bucket_flag(b) if self._mvd_guard else None
         with MK.range(f"mivod.step.{b.name}"):
             self._mv_apply(b.arena, b.i0, b.i1, gscale)
         self._mv_skip = None
@@ -476,19 +584,19 @@ class _DistributedOptimizerMixin:
             rec.add(b.name, "OPTIMIZER_STEP", t0, rec.event() if cuda else rec.host())
 
     def _mvd_guard_finish(self):
-        """synchronize() with the guard on: OR the flag across ranks (one 4-byte
-        MAX allreduce), then run every bucket's fused step with the device skip
-        flag, on the comm stream after the last bucket's collective."""
+        """synchronize() with the guard on, after the last bucket: ("step" mode)
+        run every bucket's fused update with the step's flag; then copy the flags
+        to pinned host memory for the next step's bookkeeping."""
         flag = self._mvd_flag
         if flag is None:
             return
         cuda = flag.is_cuda and self._mvd_stream is not None and not self._mvd_inline
         ctx = torch.cuda.stream(self._mvd_stream) if cuda else contextlib.nullcontext()
         with ctx:
-            if self._mvd_comm:
-                C.allreduce_(flag, C.Max)
-            for b in self._mvd_buckets:
-                self._mvd_apply_bucket(b, cuda)
+            if self._mvd_guard_mode == "step":
+                for b in self._mvd_buckets:
+                    self._mvd_apply_bucket(b, cuda)
+            self._mvd_flag_plan = list(self._mvd_buckets)
             if flag.is_cuda:
                 self._mvd_flag_host.copy_(flag, non_blocking=True)
                 self._mvd_flag_ev = torch.cuda.Event()
@@ -503,7 +611,8 @@ class _DistributedOptimizerMixin:
 
     def guard_stats(self) -> dict:
         """Overflow-guard counters (skipped steps so far, current wire scale)."""
-        return {"enabled": self._mvd_guard, "skipped_steps": self._mvd_skipped,
+        return {"enabled": self._mvd_guard, "mode": self._mvd_guard_mode,
+                "skipped_steps": self._mvd_skipped,
                 "wire_scale": self._mvd_gs, "dynamic": self._mvd_dynamic}
 
     def _mvd_expose_grads(self, b: _Bucket):

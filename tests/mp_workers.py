@@ -332,6 +332,18 @@ def hierarchical():
     _close(hvd.allreduce(x, op=hvd.Sum, name="h1"), torch.arange(7, dtype=torch.float32) * n +
            sum(range(n)))
     _close(hvd.allreduce(x, name="h2"), torch.arange(7, dtype=torch.float32) + (n - 1) / 2)
+    # Max / Min are never summed by the two-level schedule (they run flat): the
+    # Keras plan check MAX-reduces int64 hashes with hierarchical on
+    from mivod.parallel import collectives as C
+    h = torch.tensor([1000 + r, -r], dtype=torch.int64)
+    C.allreduce_(h, C.Max)
+    assert h.tolist() == [1000 + n - 1, 0], h
+    m = torch.tensor([float(r), -float(r)])
+    C.allreduce_(m, C.Min)
+    assert m.tolist() == [0.0, -float(n - 1)], m
+    m = torch.tensor([float(r)])
+    C.hierarchical_allreduce_(m, C.Max)
+    assert m.tolist() == [float(n - 1)], m
     hvd.shutdown()
     print("OK", r)
 
@@ -648,6 +660,10 @@ def adasum_vhdd():
         es = buf.element_size()
         bound = 2 * S * (n - 1) / n * es + 2 * A.LAST["levels"] * A.ALIGN * es
         assert A.LAST["exchange_bytes"] <= bound, (A.LAST, bound)
+        # Gram partials are summed inside each level's 2^(i+1) group only:
+        # (i+1) exchanges of nseg*3 fp32 at level i, independent of the world size
+        L = A.LAST["levels"]
+        assert A.LAST["dot_bytes"] == sum(i + 1 for i in range(L)) * len(sizes) * 3 * 4, A.LAST
         wire_ref = A.adasum_reference([v.to(dt).float() for v in vecs], table)
         err = (buf.float() - wire_ref).abs().max().item()
         scale = wire_ref.abs().max().item()
@@ -656,6 +672,17 @@ def adasum_vhdd():
             torch.testing.assert_close(buf, ref, rtol=2e-5, atol=2e-5 * scale)
         allb = C.allgather(buf.float().unsqueeze(0))
         assert all(torch.equal(allb[0], allb[i]) for i in range(n)), dt
+    # fresh tables with the SAME total but different segment layouts, built and
+    # dropped one after another (CPython may reuse the address): each call must
+    # use its own segment boundaries (the clipped-table cache lives on the table)
+    for lay in ([64, 128], [128, 64], [64, 128]):
+        tab = K.make_chunk_table(lay, "cpu")
+        vs = [torch.randn(192, generator=torch.Generator().manual_seed(7 + q)) * (q + 1)
+              for q in range(n)]
+        x = vs[r].clone()
+        C.allreduce_(x, C.Adasum, adasum_table=tab)
+        torch.testing.assert_close(x, A.adasum_reference(vs, tab), rtol=2e-5, atol=2e-5)
+        del tab
     # identical inputs: adasum(g, ..., g) = g ; orthogonal inputs: the sum
     g = torch.linspace(-1, 1, 300)
     t1 = K.make_chunk_table([300], "cpu")
@@ -671,12 +698,17 @@ def adasum_vhdd():
 
 
 def overflow_guard():
-    """fp16 wire + FusedSGD: rank 1 injects inf into one gradient at step 2; the
-    pack kernel flags it, the MAX-allreduced flag makes EVERY rank skip that step
-    (parameters identical across ranks and unchanged by the step), a warning is
-    logged, and training continues afterwards."""
+    """fp16 wire + FusedSGD: rank 1 injects inf into one gradient at step 2.  The
+    reduced bucket holding it is non-finite on EVERY rank (the scan of the reduced
+    bucket sets the same flag everywhere, no extra collective):
+    MIVOD_GUARD_MODE=bucket (default) skips that bucket's update on every rank
+    while the other buckets' updates (already overlapped with backward) apply;
+    MIVOD_GUARD_MODE=step skips the whole step.  Parameters stay identical
+    across ranks and finite, a warning is logged, the saved optimizer state
+    does not count a fully skipped step, and training continues afterwards."""
     import warnings
     from mivod.optim import FusedSGD
+    mode = os.environ.get("MIVOD_GUARD_MODE", "bucket")
     hvd.init()
     r, n = hvd.rank(), hvd.size()
     torch.manual_seed(0)
@@ -685,7 +717,15 @@ def overflow_guard():
                                    named_parameters=m.named_parameters(),
                                    compression=hvd.Compression.fp16,
                                    bucket_mb=0.005, first_bucket_mb=0.001)
-    assert opt.guard_stats()["enabled"]
+    gs = opt.guard_stats()
+    assert gs["enabled"] and gs["mode"] == mode
+    plan = opt.bucket_plan()
+    assert len(plan) > 1
+    names = [nm for nm, _ in m.named_parameters()]
+    first = names[0]
+    poisoned = next(i for i, (_, _, ps) in enumerate(plan) if first in ps)
+    in_poisoned = [nm in plan[poisoned][2] for nm in names]
+    assert not all(in_poisoned)
     g = torch.Generator().manual_seed(100 + r)
     x, y = torch.randn(4, 3, 8, 8, generator=g), torch.randint(0, 10, (4,), generator=g)
     snap = {}
@@ -707,8 +747,18 @@ def overflow_guard():
             torch.nn.functional.cross_entropy(m(x), y).backward()
             opt.step()
             snap[step] = (before, [p.detach().clone() for p in m.parameters()])
+            if step == 2:
+                sd = opt.state_dict()          # resolves the step-2 flags first
     b2, a2 = snap[2]
-    assert all(torch.equal(p, q) for p, q in zip(b2, a2)), "overflow step was not skipped"
+    same = [torch.equal(p, q) for p, q in zip(b2, a2)]
+    if mode == "step":
+        assert all(same), "overflow step was not skipped"
+        steps = {int(v["step"]) for v in sd["state"].values() if "step" in v}
+        assert steps == {1}, steps          # the skipped step is not counted
+    else:
+        assert all(s_ for s_, ip in zip(same, in_poisoned) if ip), "poisoned bucket applied"
+        assert not all(s_ for s_, ip in zip(same, in_poisoned) if not ip), \
+            "clean buckets were not applied"
     b3, a3 = snap[3]
     assert any(not torch.equal(p, q) for p, q in zip(b3, a3)), "training did not resume"
     assert opt.guard_stats()["skipped_steps"] == 1, opt.guard_stats()
@@ -1033,12 +1083,73 @@ def gpu_mesh():
         opt.step()
     torch.cuda.synchronize()
     assert st.mesh.mesh.calls >= calls + 3 * len(opt.bucket_plan())
+    # the bucket pack kernel wrote straight into the IPC staging slot (no copy)
+    assert st.mesh.mesh.copies_saved >= 3 * len(opt.bucket_plan()), st.mesh.stats()
+    if int(os.environ.get("MIVOD_MESH_ONESHOT_KB", "1024")) < 64:
+        assert st.mesh.mesh.two_shot_calls > 0, st.mesh.stats()
     flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
     allf = hvd.allgather(flat.unsqueeze(0))
     assert torch.equal(allf[0], allf[-1])
     assert st.mesh.status() == 0
     hvd.shutdown()
     print("OK", r)
+
+
+def gpu_mesh_timeout():
+    """A peer that never arrives: rank 1 skips the mesh allreduce.  Rank 0's
+    kernel waits MIVOD_MESH_TIMEOUT_S, poisons the output with NaN, sets the
+    host-mapped status word, and the native watcher ends rank 0 with a
+    diagnosis (exit 1).  Rank 1 sits in a gloo barrier and fails when rank 0's
+    connection drops: both ranks exit non-zero, nobody trains on a local gradient."""
+    import time
+    import torch.distributed as dist
+    from mivod.common import basics as B
+    from mivod.parallel import collectives as C
+    hvd.init()
+    r = hvd.rank()
+    dev = hvd.device()
+    st = B.state()
+    assert st.mesh is not None and st.mesh.mesh.timeout_s <= 5
+    if r == 0:
+        x = torch.ones(1000, device=dev)
+        C.allreduce_(x, C.Sum)
+        torch.cuda.synchronize()
+        time.sleep(20)              # the watcher exits the process long before this
+        print("rank 0 was not stopped by the mesh watcher", flush=True)
+        sys.exit(0)
+    dist.barrier(group=st.cpu_pg)   # never completes: rank 0 dies
+    print("rank 1 passed a barrier rank 0 never reached", flush=True)
+    sys.exit(0)
+
+
+def gpu_mesh_timeout_raise():
+    """MIVOD_MESH_TIMEOUT_EXIT=0: the timed-out allreduce leaves NaN in the output
+    (not the local gradient), status() reports it, and every later mesh call raises."""
+    import time
+    import torch.distributed as dist
+    from mivod.common import basics as B
+    from mivod.parallel import collectives as C
+    hvd.init()
+    r = hvd.rank()
+    dev = hvd.device()
+    st = B.state()
+    if r == 0:
+        x = torch.ones(1000, device=dev)
+        C.allreduce_(x, C.Sum)
+        torch.cuda.synchronize()
+        assert bool(torch.isnan(x).all()), x[:8]
+        t0 = time.time()
+        while not st.mesh.mesh.failed() and time.time() - t0 < 5:
+            time.sleep(0.02)
+        assert st.mesh.status() == 1 and st.mesh.mesh.failed()
+        try:
+            C.allreduce_(torch.ones(8, device=dev), C.Sum)
+            raise AssertionError("a failed mesh accepted another allreduce")
+        except RuntimeError as e:
+            assert "timed out" in str(e), e
+    dist.barrier(group=st.cpu_pg)
+    print("OK", r, flush=True)
+    os._exit(0)                     # skip shutdown: the mesh epochs are out of step
 
 
 def gpu_mesh_bench():

@@ -237,10 +237,13 @@ def test_conv1x1_kernel_matches_fp32(cuda, n, c, k, h, w, s):
     torch.testing.assert_close(part.sum(0)[0], d.sum(0), rtol=1e-4, atol=1e-2)
 
 
-@pytest.mark.parametrize("n", [1, 3])
-def test_stem_kernel_matches_fp32(cuda, n):
+@pytest.mark.parametrize("n,grid", [(1, 0), (3, 0), (3, 1), (3, 7), (5, 200), (8, 1000)])
+def test_stem_kernel_matches_fp32(cuda, n, grid):
     """mv_stem.hip: 7x7/2/pad-3 stem conv (4-channel NHWC image) vs fp32 F.conv2d, and its
-    BN-statistics partials vs the statistics of its own bf16 output."""
+    BN-statistics partials vs the statistics of its own bf16 output — with the
+    occupancy-sized grid (0) and forced persistent grids smaller and larger than the
+    row-pair count (N*56), i.e. workgroups with many rows, one row, or none (round-2
+    NaN regression: the result must not depend on the grid or the register allocation)."""
     nat = _nat()
     g = torch.Generator(device=cuda).manual_seed(n)
     x = torch.rand(n, 4, 224, 224, device=cuda, generator=g)
@@ -248,8 +251,10 @@ def test_stem_kernel_matches_fp32(cuda, n):
     x = _cl(x.to(torch.bfloat16))
     w = _cl((torch.randn(64, 4, 7, 7, device=cuda, generator=g) * 0.05).to(torch.bfloat16))
     shift = torch.randn(64, device=cuda, generator=g) * 0.1
-    z, part = nat.stem_fwd(x, w, shift)
+    z, part = nat.stem_fwd(x, w, shift, grid)
     assert z.shape == (n, 64, 112, 112) and z.is_contiguous(memory_format=torch.channels_last)
+    assert grid == 0 or part.shape[0] == grid
+    assert bool(torch.isfinite(z).all()) and bool(torch.isfinite(part).all())
     ref = F.conv2d(x.float(), w.float(), None, 2, 3)
     torch.testing.assert_close(z.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
     d = (z.float() - shift[None, :, None, None]).permute(1, 0, 2, 3).reshape(64, -1)

@@ -19,7 +19,7 @@ def free_port():
     return p
 
 
-def run_ranks(scenario, n=2, timeout=240, extra_env=None, local_size=None):
+def run_ranks(scenario, n=2, timeout=240, extra_env=None, local_size=None, expect_ok=True):
     port = free_port()
     procs = []
     for r in range(n):
@@ -44,6 +44,8 @@ def run_ranks(scenario, n=2, timeout=240, extra_env=None, local_size=None):
         for p in procs:
             if p.poll() is None:
                 p.kill()
+    if not expect_ok:
+        return [p.returncode for p in procs], outs
     for r, (p, out) in enumerate(zip(procs, outs)):
         assert p.returncode == 0 and f"OK {r}" in out, f"rank {r} rc={p.returncode}\n{out}"
     return outs
@@ -139,8 +141,12 @@ def test_adasum_vector_halving_2ranks():
     run_ranks("adasum_vhdd", 2)
 
 
-def test_overflow_guard_skips_step_on_every_rank():
+def test_overflow_guard_skips_bucket_on_every_rank():
     run_ranks("overflow_guard", 2)
+
+
+def test_overflow_guard_step_mode_skips_whole_step():
+    run_ranks("overflow_guard", 2, extra_env={"MIVOD_GUARD_MODE": "step"})
 
 
 def test_timeline_records_bucket_phases(tmp_path):

@@ -46,6 +46,32 @@ def test_gpu_xgmi_mesh_one_shot_allreduce(cuda):
               extra_env={"MIVOD_TRANSPORT": "gloo-gpu", "MIVOD_MESH_MAX_MB": "1"})
 
 
+def test_gpu_xgmi_mesh_two_shot_and_staged_pack(cuda):
+    """K7 two-shot (mesh reduce-scatter + all-gather through IPC result buffers)
+    for every bucket above 1 KB, and the bucket pack writing straight into the
+    mesh staging slot: bitwise equal to the gloo wire, ranks identical."""
+    run_ranks("gpu_mesh", 2, timeout=180,
+              extra_env={"MIVOD_TRANSPORT": "gloo-gpu", "MIVOD_MESH_MAX_MB": "1",
+                         "MIVOD_MESH_ONESHOT_KB": "1"})
+
+
+def test_gpu_xgmi_mesh_timeout_exits_both_ranks(cuda):
+    """A rank that never arrives: the waiting rank's mesh kernel times out, poisons
+    its output and the watcher exits the process; the other rank then fails too."""
+    rcs, outs = run_ranks("gpu_mesh_timeout", 2, timeout=120, expect_ok=False,
+                          extra_env={"MIVOD_TRANSPORT": "gloo-gpu", "MIVOD_MESH_MAX_MB": "1",
+                                     "MIVOD_MESH_TIMEOUT_S": "3"})
+    assert rcs[0] != 0 and rcs[1] != 0, (rcs, outs)
+    assert "did not arrive within" in outs[0], outs[0]
+    assert "was not stopped" not in outs[0] and "passed a barrier" not in outs[1]
+
+
+def test_gpu_xgmi_mesh_timeout_poisons_and_raises(cuda):
+    run_ranks("gpu_mesh_timeout_raise", 2, timeout=120,
+              extra_env={"MIVOD_TRANSPORT": "gloo-gpu", "MIVOD_MESH_MAX_MB": "1",
+                         "MIVOD_MESH_TIMEOUT_S": "2", "MIVOD_MESH_TIMEOUT_EXIT": "0"})
+
+
 def test_gpu_rccl_cta_config_and_autotune(cuda):
     """ncclCommInitRankConfig with a CTA range, and the CTA autotune loop over real
     communicators (world 1: the sweep mechanics, not the timing, are what is tested)."""
