@@ -5,6 +5,7 @@
 #include "controller.h"
 #include "loop.h"
 #include "ring.h"
+#include "store.h"
 #include "timeline.h"
 
 namespace py = pybind11;
@@ -62,6 +63,51 @@ PYBIND11_MODULE(_mvcore, m) {
       .def_property_readonly("events_written", &Timeline::events_written);
 
   // CPU data plane: ring collectives over TCP on raw host pointers (tensor.data_ptr())
+  // rendezvous key-value store (launcher-hosted server, one client per rank)
+  py::class_<KVServer>(m, "KVServer")
+      .def(py::init<const std::string&, int>(), py::arg("host") = "0.0.0.0", py::arg("port") = 0)
+      .def_property_readonly("port", &KVServer::port)
+      .def_property_readonly("requests", &KVServer::requests)
+      .def("close", &KVServer::close, py::call_guard<py::gil_scoped_release>());
+  py::class_<KVClient>(m, "KVClient")
+      .def(py::init([](const std::string& host, int port, double timeout_s) {
+             py::gil_scoped_release nogil;
+             return std::make_unique<KVClient>(host, port, timeout_s);
+           }),
+           py::arg("host"), py::arg("port"), py::arg("timeout_s") = 300.0)
+      .def("set",
+           [](KVClient& c, const std::string& k, py::bytes v) {
+             std::string s = v;
+             py::gil_scoped_release nogil;
+             c.set(k, s);
+           })
+      .def("get",
+           [](KVClient& c, const std::string& k) {
+             std::string v;
+             {
+               py::gil_scoped_release nogil;
+               v = c.get(k);
+             }
+             return py::bytes(v);
+           })
+      .def("add", &KVClient::add, py::call_guard<py::gil_scoped_release>())
+      .def("check", &KVClient::check, py::call_guard<py::gil_scoped_release>())
+      .def("wait", &KVClient::wait, py::call_guard<py::gil_scoped_release>())
+      .def("delete_key", &KVClient::remove, py::call_guard<py::gil_scoped_release>())
+      .def("num_keys", &KVClient::num_keys, py::call_guard<py::gil_scoped_release>())
+      .def("compare_set",
+           [](KVClient& c, const std::string& k, py::bytes e, py::bytes d) {
+             std::string es = e, ds = d, v;
+             {
+               py::gil_scoped_release nogil;
+               v = c.compare_set(k, es, ds);
+             }
+             return py::bytes(v);
+           })
+      .def("set_timeout", &KVClient::set_timeout)
+      .def_property_readonly("timeout", &KVClient::timeout)
+      .def("close", &KVClient::close, py::call_guard<py::gil_scoped_release>());
+
   py::class_<Ring>(m, "Ring")
       .def(py::init<int, int, double>(), py::arg("rank"), py::arg("size"),
            py::arg("timeout_s") = 300.0)

@@ -91,86 +91,6 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restri
   *reinterpret_cast<u32x2*>(idx + t * 8) = u32x2{lo, hi};
 }
 
-// 3x3 / stride 2 / pad 1 forward on a 2x2 block of outputs per lane (even OH, OW; H = 2 OH,
-// W = 2 OW): the block's windows cover a 5x5 input patch, so 25 loads + BN/ReLU per 4 outputs
-// instead of 36.  Rows are visited top to bottom and columns left to right, so every
-// output still scans its own window in (kh, kw) order: same first-maximum argmax as above.
-__global__ __launch_bounds__(256) void maxpool_fwd_k3s2_kernel(const __bf16* __restrict__ x,
-                                                               const float* __restrict__ scale,
-                                                               const float* __restrict__ bias,
-                                                               int relu, __bf16* __restrict__ y,
-                                                               uint8_t* __restrict__ idx,
-                                                               PoolGeo g) {
-  const uint32_t cv = (uint32_t)g.C / 8, hb = (uint32_t)g.OH / 2, wb = (uint32_t)g.OW / 2;
-  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-  if (t >= (uint32_t)g.N * hb * wb * cv) return;
-  const uint32_t q0 = t / cv;
-  const int c = (int)(t - q0 * cv) * 8;
-  const uint32_t q1 = q0 / wb;
-  const int b = (int)(q0 - q1 * wb);
-  const uint32_t n = q1 / hb;
-  const int a = (int)(q1 - n * hb);
-  float sc[8], bi[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { sc[j] = 1.f; bi[j] = 0.f; }
-  if (scale) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { sc[j] = scale[c + j]; bi[j] = bias[c + j]; }
-  }
-  float best[4][8];
-  uint32_t arg[4][8];
-#pragma unroll
-  for (int o = 0; o < 4; ++o)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { best[o][j] = -INFINITY; arg[o][j] = 0; }
-  const int h0 = 4 * a - 1, w0 = 4 * b - 1;
-#pragma unroll
-  for (int lr = 0; lr < 5; ++lr) {
-    const int ih = h0 + lr;
-    if (ih < 0 || ih >= g.H) continue;
-#pragma unroll
-    for (int lc = 0; lc < 5; ++lc) {
-      const int iw = w0 + lc;
-      if (iw < 0 || iw >= g.W) continue;
-      float v[8];
-      load8(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c, v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float e = scale ? __builtin_fmaf(v[j], sc[j], bi[j]) : v[j];
-        if (relu) e = e > 0.f ? e : 0.f;
-        v[j] = (float)(__bf16)e;
-      }
-#pragma unroll
-      for (int da = 0; da < 2; ++da) {
-        const int kh = lr - 2 * da;
-        if (kh < 0 || kh > 2) continue;
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const int kw = lc - 2 * db;
-          if (kw < 0 || kw > 2) continue;
-          const int o = 2 * da + db;
-          const uint32_t pos = (uint32_t)(kh * 3 + kw);
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (v[j] > best[o][j] || __builtin_isnan(v[j])) {
-              best[o][j] = v[j];
-              arg[o][j] = pos;
-            }
-        }
-      }
-    }
-  }
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-  for (int o = 0; o < 4; ++o) {
-    const int64_t op = (((int64_t)n * g.OH + 2 * a + (o >> 1)) * g.OW + 2 * b + (o & 1)) * g.C + c;
-    store8(y + op, best[o]);
-    const uint32_t lo = arg[o][0] | (arg[o][1] << 8) | (arg[o][2] << 16) | (arg[o][3] << 24);
-    const uint32_t hi = arg[o][4] | (arg[o][5] << 8) | (arg[o][6] << 16) | (arg[o][7] << 24);
-    *reinterpret_cast<u32x2*>(idx + op) = u32x2{lo, hi};
-  }
-}
-
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restrict__ dy,
                                                           const __bf16* __restrict__ dy2,
                                                           const uint8_t* __restrict__ idx,
@@ -471,18 +391,10 @@ void mv_maxpool_fwd(const void* x, const float* scale, const float* bias, bool r
   const int64_t total = (int64_t)N * OH * OW * (C / 8);
   if (total >= (int64_t(1) << 32)) return;   // bindings reject such shapes first
   if (!total) return;
-  // opt-in (MIVOD_POOL_FWD_BLOCK=1): bench A/B level with the per-output kernel at bs 2048
-  // (15,334 / 15,331 vs 15,319 / 15,344 img/s) — the 4-output register state costs what the
-  // saved loads gain
-  static const bool blk = [] {
-    const char* e = std::getenv("MIVOD_POOL_FWD_BLOCK");
-    return e && e[0] == '1';
-  }();
-  if (blk && k == 3 && s == 2 && p == 1 && OH % 2 == 0 && OW % 2 == 0 && H == 2 * OH &&
-      W == 2 * OW)
-    hipLaunchKernelGGL(maxpool_fwd_k3s2_kernel, dim3(blocks_for(total / 4)), dim3(256), 0, st,
-                       (const __bf16*)x, scale, bias, relu ? 1 : 0, (__bf16*)y, idx, g);
-  else if (k == 3)
+  // (a 2x2-output-block variant, 25 loads per 4 outputs, measured level with this
+  // per-output kernel at bs 2048 — 15,334 / 15,331 vs 15,319 / 15,344 img/s — and was
+  // removed in round 3)
+  if (k == 3)
     hipLaunchKernelGGL(maxpool_fwd_kernel<3>, dim3(blocks_for(total)), dim3(256), 0, st,
                        (const __bf16*)x, scale, bias, relu ? 1 : 0, (__bf16*)y, idx, g);
   else

@@ -67,6 +67,7 @@ class _State:
         self.init_count = 0
         self.owns_pg = False
         self.engine = None
+        self.store_kind = "none"  # rendezvous: "native" (launcher's KV store) | "torch"
         self.lock = threading.RLock()
 
 
@@ -176,9 +177,18 @@ def init(comm=None, process_sets=None):
                 backend = "nccl" if (use_gpu and transport == "torch") else "gloo"
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29500")
+                tmo = float(os.environ.get("MIVOD_INIT_TIMEOUT_S", "600"))
                 kwargs = dict(backend=backend, rank=_state.rank, world_size=_state.size,
-                              timeout=datetime.timedelta(
-                                  seconds=float(os.environ.get("MIVOD_INIT_TIMEOUT_S", "600"))))
+                              timeout=datetime.timedelta(seconds=tmo))
+                # launched by mivodrun: bootstrap through the launcher's native
+                # rendezvous store (csrc/engine/store.cc) instead of torch's TCPStore
+                from ..run.store import from_env as _native_store
+                store = _native_store(tmo)
+                if store is not None:
+                    kwargs["store"] = store
+                    _state.store_kind = "native"
+                else:
+                    _state.store_kind = "torch"
                 if backend == "nccl":
                     kwargs["device_id"] = _state.device
                 dist.init_process_group(**kwargs)

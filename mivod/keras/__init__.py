@@ -9,11 +9,15 @@ U20/U21, §2.6), as used by /root/reference/mnist_keras.py:20,30,87,97 and
 subclass of the optimizer's own class (same class name, so saved models load
 with the plain ``load_model`` as the reference does at mnist_keras.py:124),
 re-instantiated from ``opt.get_config()``, whose ``get_gradients`` averages the
-gradients across ranks when ``size() > 1``.  The averaging runs on a STATIC
-schedule (``_static.StaticGradientReducer``): the plan — one fusion buffer per
-(device, dtype), checked across ranks once — is built on the first step, and
-every step then packs (K1 pack kernel on GPU), reduces once per group over RCCL
-(native TCP ring / gloo on CPU) and unpacks, with no per-step negotiation.
+gradients across ranks when ``size() > 1``, on a STATIC schedule checked across
+ranks once (no per-step negotiation).  On GPU the averaging OVERLAPS the
+backward pass (``_static.OverlappedGradientReducer``): tensor hooks armed
+during ``torch.autograd.grad`` pack each completed bucket (K1 kernel) and the
+high-priority comm stream reduces it over RCCL while autograd continues; the
+result is zero-copy views into the reduced buckets.  On CPU, or with gradient
+clipping, ``_static.StaticGradientReducer`` packs, reduces once per (device,
+dtype) group (native TCP ring / gloo) and unpacks after the backward.
+``MIVOD_KERAS_OVERLAP=0/1`` forces the choice.
 ``MIVOD_KERAS_NEGOTIATED=1`` submits every gradient to the negotiated engine under
 ``<Name>_Allreduce/<i>`` instead (horovod's per-tensor protocol).
 """
@@ -40,13 +44,26 @@ class _DistributedOptimizerMixin:
         self._hvd_compression = compression
         self._hvd_sparse_as_dense = sparse_as_dense
         self._hvd_op = op
-        from ._static import StaticGradientReducer
+        from ._static import OverlappedGradientReducer, StaticGradientReducer
         self._hvd_static = StaticGradientReducer(self._hvd_name, op, compression)
+        self._hvd_overlap = OverlappedGradientReducer(self._hvd_name, op, compression)
+
+    def _hvd_overlappable(self, params) -> bool:
+        env = os.environ.get("MIVOD_KERAS_OVERLAP", "")
+        if env == "0" or os.environ.get("MIVOD_KERAS_NEGOTIATED", "0") == "1":
+            return False
+        if self.clipnorm is not None or self.clipvalue is not None:
+            return False        # Keras clips the LOCAL gradients before the average
+        return env == "1" or (len(params) > 0 and params[0].is_cuda)
 
     def get_gradients(self, loss, params):
-        grads = super().get_gradients(loss, params)
         if size() <= 1:
-            return grads
+            return super().get_gradients(loss, params)
+        params = list(params)
+        if self._hvd_overlappable(params):
+            # the reduction overlaps the backward pass (hooks + comm stream)
+            return self._hvd_overlap(loss, params)
+        grads = super().get_gradients(loss, params)
         if os.environ.get("MIVOD_KERAS_NEGOTIATED", "0") != "1":
             return self._hvd_static(grads)
         handles = []

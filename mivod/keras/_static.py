@@ -100,3 +100,180 @@ class StaticGradientReducer:
             for i, r in zip(g.idx, res):
                 out[i] = r
         return out
+
+
+class OverlappedGradientReducer:
+    """GPU path of the Keras ``DistributedOptimizer.get_gradients``: the gradient
+    reduction overlaps the backward pass, as mivod.torch.DistributedOptimizer's
+    hook path does (BASELINE.json north star: "gradient tensors from the TF2-Keras
+    and PyTorch-ROCm backward hooks ... overlapped with backward on a side HIP
+    stream").
+
+    The plan (built once, checked across ranks like StaticGradientReducer's):
+    the variables in backward order split into buckets (``MIVOD_FIRST_BUCKET_MB``
+    / ``MIVOD_BUCKET_MB`` / ``MIVOD_LAST_BUCKET_MB``, the torch planner), one
+    persistent fusion buffer per (device, wire dtype).  Per step:
+
+    * ``torch.autograd.grad`` runs with a tensor hook armed on every variable;
+      a hook stores its gradient and, when its bucket is complete, the K1 pack
+      kernel copies the bucket into the fusion buffer on the compute stream and
+      the comm stream (high priority) waits for the pack and runs the bucket's
+      collective — while autograd keeps computing earlier layers' gradients;
+    * buckets whose variables got no gradient (unused) reduce zeros after
+      autograd returns;
+    * the compute stream waits for the comm stream; the result is zero-copy
+      views into the reduced buffers (wire dtype == variable dtype) or the K2
+      unpack kernel's decompressed copies.
+
+    The returned views are overwritten by the next step's reduction (Keras applies
+    them in the same step).  Gradient clipping (clipnorm / clipvalue: applied to
+    the LOCAL gradients before the average, as Keras' get_gradients does) keeps
+    the unfused StaticGradientReducer path."""
+
+    def __init__(self, name: str, op: int, compression):
+        self.name = name
+        self.op = op
+        self.compression = compression
+        self.key = None
+        self.plans = 0
+        self.steps = 0
+        self.launched_in_backward = 0     # buckets whose collective started inside autograd
+        self._armed = False
+        self._hooks = []
+        self._params: List[torch.nn.Parameter] = []
+
+    # ----------------------------------------------------------------- plan
+    def _plan(self, key, params) -> None:
+        from ..common import basics
+        from ..torch.optimizer import _GradArena, plan_buckets
+        StaticGradientReducer._check_across_ranks(self, key)
+        for h in self._hooks:
+            h.remove()
+        cfg = basics.state().config
+        self._params = list(params)
+        pos = {id(p): i for i, p in enumerate(reversed(self._params))}
+        by = {}
+        for p in reversed(self._params):                  # backward order
+            by.setdefault((p.dtype, p.device), []).append(p)
+        arenas = [_GradArena(ps, self.compression.wire_dtype(dt) if dt.is_floating_point else dt)
+                  for (dt, _), ps in by.items()]
+        mb = 2 ** 20
+        self.buckets = plan_buckets(arenas, int(cfg.first_bucket_mb * mb), int(cfg.bucket_mb * mb),
+                                    pos, int(cfg.last_bucket_mb * mb))
+        self.where = {}
+        for b in self.buckets:
+            for k, p in enumerate(b.params):
+                self.where[id(p)] = (b, b.i0 + k)
+        self.tables = {}
+        self._hooks = [p.register_hook(self._make_hook(p)) for p in self._params]
+        self.key = key
+        self.plans += 1
+
+    def _make_hook(self, p):
+        def hook(g):
+            if self._armed:
+                self._ready(p, g)
+            return None
+        return hook
+
+    # ------------------------------------------------------------- hot path
+    def _ready(self, p, g):
+        b, i = self.where[id(p)]
+        self._grads[(id(b.arena), i)] = g
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch_ready(inside_backward=True)
+
+    def _launch_ready(self, inside_backward: bool):
+        while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
+            self._launch(self.buckets[self._next], inside_backward)
+            self._next += 1
+
+    def _launch(self, b, inside_backward: bool):
+        from ..common import basics
+        from ..utils import timeline as TL
+        a = b.arena
+        ts, offs = [], []
+        with torch.no_grad():
+            for k, p in enumerate(b.params):
+                i = b.i0 + k
+                g = self._grads.get((id(a), i))
+                lo = a.offsets[i]
+                if g is None:
+                    a.grad[lo:lo + p.numel()].zero_()
+                    continue
+                if not K.is_dense(g):
+                    g = g.contiguous()
+                ts.append(g)
+                offs.append(lo)
+            if ts:
+                K.pack(ts, a.grad, offs)
+        flat = a.grad[b.lo:b.hi]
+        st = basics.state()
+        stream = st.comm_stream if flat.is_cuda else None
+        rec = TL.recorder()
+        if stream is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            ctx = torch.cuda.stream(stream)
+        else:
+            import contextlib
+            ctx = contextlib.nullcontext()
+        with ctx:
+            if stream is not None:
+                stream.wait_event(ev)
+            t0 = (rec.event() if stream is not None else rec.host()) if rec is not None else None
+            table = None
+            if self.op == C.Adasum:
+                table = a.table(b.i0, b.i1)
+            C.allreduce_(flat, self.op, adasum_table=table)
+            if rec is not None:
+                rec.add(f"{self.name}.{b.name}",
+                        "ADASUM" if self.op == C.Adasum else
+                        ("NCCL_ALLREDUCE" if stream is not None else "RING_ALLREDUCE"),
+                        t0, rec.event() if stream is not None else rec.host())
+        if inside_backward:
+            self.launched_in_backward += 1
+
+    def __call__(self, loss, params) -> List[torch.Tensor]:
+        from ..common import basics
+        params = list(params)
+        key = tuple((i, str(p.dtype), tuple(p.shape), p.device.type) for i, p in enumerate(params))
+        if key != self.key:
+            self._plan(key, params)
+        for b in self.buckets:
+            b.pending = len(b.params)
+        self._next = 0
+        self._grads = {}
+        self._armed = True
+        try:
+            raw = torch.autograd.grad(loss, params, allow_unused=True)
+        finally:
+            self._armed = False
+        for b in self.buckets:                 # unused variables: reduce zeros
+            b.pending = 0
+        self._launch_ready(inside_backward=False)
+        st = basics.state()
+        if st.comm_stream is not None and params and params[0].is_cuda:
+            torch.cuda.current_stream().wait_stream(st.comm_stream)
+        out: List[Optional[torch.Tensor]] = [None] * len(params)
+        index = {id(p): j for j, p in enumerate(params)}
+        for b in self.buckets:
+            a = b.arena
+            same = a.grad.dtype == a.dtype
+            outs, offs = [], []
+            for k, p in enumerate(b.params):
+                i = b.i0 + k
+                if same:
+                    out[index[id(p)]] = a.slot(a.grad, i)
+                else:
+                    t = torch.empty_like(p)
+                    outs.append(t)
+                    offs.append(a.offsets[i])
+                    out[index[id(p)]] = t
+            if outs:
+                K.unpack(outs, a.grad, offs)
+        self._grads = {}
+        self.steps += 1
+        del raw
+        return out

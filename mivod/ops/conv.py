@@ -147,15 +147,7 @@ class _Conv1x1BN(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             slot, ctx.slot = ctx.slot, None
-            if (slot is not None and slot.bn is not None and slot.mode == 1
-                    and slot.pending is None):
-                # x = relu(bn(z)): mivod's implicit-GEMM kernel (ks = 1) with the BN+ReLU
-                # backward reduce in its epilogue, as _Conv3x3's stride-1 data gradient
-                from . import kernels as K
-                xb, _, vec = slot.bn
-                slot.pending = tuple(K.native().conv3x3_bn_bwd(dy, _transposed_filter(w), xb,
-                                                               vec))
-            elif (slot is not None and slot.bn is not None and slot.grad is not None
+            if (slot is not None and slot.bn is not None and slot.grad is not None
                     and slot.pending is None):
                 from . import kernels as K
                 n, cin, h, wd = x.shape
@@ -190,10 +182,10 @@ def bwd_fusable(m: nn.Conv2d, x: torch.Tensor):
     """GradSlot of x's producer when this 1x1 conv's data gradient can carry that
     producer's BN backward reduce; else None.  Mode 3 (BN+add+ReLU, block input): the
     streaming GEMM with the bitmask/shortcut epilogue (Cout = the GEMM's K in {64, 128,
-    256}).  Mode 1 (BN+ReLU, a bottleneck's conv3 input): the implicit-GEMM conv kernel
-    with ks = 1 and the BN+ReLU reduce epilogue — opt-in (MIVOD_CONV1X1_BN_BWD=1): on the
-    ResNet-50 bs2048 conv3 shapes it is level with MIOpen dgrad + BN2 backward on layer1 and
-    5-14% behind on layers 2-4 (scripts/micro_dgrad_bn.py), bench A/B neutral."""
+    256}).  (A mode-1 variant — conv3's data gradient as the implicit-GEMM kernel with
+    ks = 1 carrying BN2's reduce — measured level on layer1 and 5-14% behind on layers 2-4
+    (scripts/micro_dgrad_bn.py), bench A/B neutral, and was removed in round 3; the BN3
+    fold computes conv3's data gradient itself.)"""
     slot = getattr(x, "_mv_slot", None)
     if (slot is None or getattr(slot, "bn", None) is None
             or os.environ.get("MIVOD_CONV_BN_BWD_FUSE", "1") == "0"
@@ -203,8 +195,6 @@ def bwd_fusable(m: nn.Conv2d, x: torch.Tensor):
         return None
     mode = getattr(slot, "mode", 0)
     if mode == 3 and m.out_channels in (64, 128, 256):
-        return slot
-    if mode == 1 and os.environ.get("MIVOD_CONV1X1_BN_BWD", "0") == "1":
         return slot
     return None
 

@@ -267,8 +267,9 @@ def exported_env(exports: Sequence[str]) -> Dict[str, str]:
     return env
 
 
-def rank_env(slot: Slot, size: int, master_addr: str, master_port: int) -> Dict[str, str]:
-    return {
+def rank_env(slot: Slot, size: int, master_addr: str, master_port: int,
+             store_port: int = 0) -> Dict[str, str]:
+    env = {
         "HOROVOD_RANK": str(slot.rank), "HOROVOD_SIZE": str(size),
         "HOROVOD_LOCAL_RANK": str(slot.local_rank), "HOROVOD_LOCAL_SIZE": str(slot.local_size),
         "HOROVOD_CROSS_RANK": str(slot.cross_rank), "HOROVOD_CROSS_SIZE": str(slot.cross_size),
@@ -278,6 +279,12 @@ def rank_env(slot: Slot, size: int, master_addr: str, master_port: int) -> Dict[
         "MASTER_ADDR": master_addr, "MASTER_PORT": str(master_port),
         "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
     }
+    if store_port:
+        # the launcher-hosted native rendezvous store (csrc/engine/store.cc), under
+        # horovodrun's Gloo rendezvous variable names
+        env["HOROVOD_GLOO_RENDEZVOUS_ADDR"] = master_addr
+        env["HOROVOD_GLOO_RENDEZVOUS_PORT"] = str(store_port)
+    return env
 
 
 def _is_local(host: str) -> bool:
@@ -337,6 +344,17 @@ def launch(slots: List[Slot], command: List[str], extra_env: Dict[str, str],
     if all(_is_local(s.host) for s in slots):
         master_addr = "127.0.0.1"
     master_port = master_port or _free_port()
+    server = None
+    store_port = 0
+    if os.environ.get("MIVOD_STORE", "native") != "torch":
+        try:
+            from .store import serve
+            server = serve("127.0.0.1" if master_addr == "127.0.0.1" else "0.0.0.0", 0)
+            store_port = server.port
+        except Exception as e:     # no native core: ranks fall back to torch's TCPStore
+            if verbose:
+                print(f"[mivodrun] native rendezvous store unavailable ({e}); using "
+                      "torch's TCPStore", file=sys.stderr)
     procs: List[subprocess.Popen] = []
     pumps = []
     tag = tag_output if tag_output is not None else size > 1   # default: tag when N > 1
@@ -344,12 +362,12 @@ def launch(slots: List[Slot], command: List[str], extra_env: Dict[str, str],
     for s in slots:
         env = dict(os.environ)
         env.update(extra_env)
-        env.update(rank_env(s, size, master_addr, master_port))
+        env.update(rank_env(s, size, master_addr, master_port, store_port))
         if _is_local(s.host):
             cmd, penv = command, env
         else:
             renv = dict(extra_env)
-            renv.update(rank_env(s, size, master_addr, master_port))
+            renv.update(rank_env(s, size, master_addr, master_port, store_port))
             cmd, penv = ssh_command(s.host, renv, command, cwd, ssh_port), dict(os.environ)
         if verbose:
             print(f"[mivodrun] rank {s.rank} on {s.host}: {' '.join(cmd)}", file=sys.stderr)
@@ -405,6 +423,8 @@ def launch(slots: List[Slot], command: List[str], extra_env: Dict[str, str],
         signal.signal(signal.SIGTERM, old_term)
         for t in pumps:
             t.join(timeout=5)
+        if server is not None:
+            server.close()
     return rc
 
 

@@ -69,32 +69,14 @@ __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
   *reinterpret_cast<f32x4*>(p) = a;
   *reinterpret_cast<f32x4*>(p + 4) = b;
 }
-// Packed RNE f32x2 -> bf16x2 on gfx950 (lo <- a, hi <- b).  Two forms:
-//
-// cvt_pk_bf16: inline asm.  NOT __builtin_convertvector(f32x2 -> bf16x2): ROCm 7.2
-//   clang mis-lowers that inside unrolled loops (only the even elements converted:
-//   caught by tests/test_kernels_gpu.py::test_pack_unpack_cast_scale).  The compiler's
-//   hazard recognizer cannot see into inline asm, so its inputs must NOT be fresh MFMA
-//   results in VGPRs: CDNA needs 11 wait states (16x16x32) between an MFMA writing a
-//   VGPR and a VALU reading it and does not interlock.  Every use in mivod reads values
-//   that went through VALU epilogue math or an accvgpr read first —
-//   scripts/check_mfma_asm_hazards.py (tests/test_kernel_asm_hazards.py) verifies that
-//   for every kernel.  (Round 2's stem_fwd_kernel NaN at __launch_bounds__(256, 2) was
-//   this hazard: its accumulators moved to VGPRs and were converted 0-6 wait states
-//   after the MFMA.)
-// cvt_pk_bf16_cc: compiler-selected (a two-element build of scalar casts), hazard-safe
-//   on raw MFMA accumulators — used there.  Not used everywhere: in the conv3x3 / GEMM
-//   epilogues it changed the register allocation and cost the 128x128 conv3x3 tiles
-//   ~45% (7.6 -> 11.1 ms/step at bs 2048, round-3 A/B, gpurun_out/ab_new.md).
+// Packed RNE f32x2 -> bf16x2 on gfx950 (lo <- a, hi <- b).  Written as inline
+// asm: ROCm 7.2 clang mis-lowers __builtin_convertvector(f32x2 -> bf16x2) inside
+// unrolled loops (it converted only the even elements: caught by
+// tests/test_kernels_gpu.py::test_pack_unpack_cast_scale).
 __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
   uint32_t r;
   asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
-}
-__device__ __forceinline__ uint32_t cvt_pk_bf16_cc(float a, float b) {
-  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-  const bf16x2_t v = {(__bf16)a, (__bf16)b};
-  return __builtin_bit_cast(uint32_t, v);
 }
 
 __device__ __forceinline__ void store8(__bf16* p, const float (&v)[8]) {

@@ -43,13 +43,10 @@ __device__ __forceinline__ f32x4v mfma(const bf16x8& a, const bf16x8& b, const f
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// 2 waves/SIMD: 236 VGPRs with the MFMA accumulators in VGPRs (1.21 vs 1.53 ms at 1 wave).
-// Round 2 saw NaN at this bound: the epilogue's bf16 conversion was inline asm, which
-// the compiler's hazard recognizer cannot see into, so it read the VGPR accumulators 0-6
-// wait states after the MFMA wrote them (11 needed; no hardware interlock) — the
-// epilogue now uses mv_common.h's compiler-selected cvt_pk_bf16_cc; checked by
-// scripts/check_mfma_asm_hazards.py; tests/test_conv_gpu.py runs several grid sizes.
-__global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const __bf16* __restrict__ x,
+// NOTE (round 2): __launch_bounds__(256, 2) compiles this kernel to 236 VGPRs with the MFMA
+// accumulators in VGPRs (2 waves/SIMD, 1.21 vs 1.53 ms) but produced wrong outputs (NaN)
+// in test_stem_kernel_matches_fp32 on gfx950 — not understood yet; kept at 1 wave/SIMD.
+__global__ __launch_bounds__(256) void stem_fwd_kernel(const __bf16* __restrict__ x,
                                                        const __bf16* __restrict__ w,
                                                        __bf16* __restrict__ z,
                                                        const float* __restrict__ shift,
@@ -140,9 +137,8 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const __bf16* __restri
     for (int t = 0; t < 7; ++t) {
       __bf16* zr = z + (row * kR + j) * (int64_t)kOW * kCO + 16 * wv + 4 * g;
       const int p = t * 16 + rl;
-      // raw MFMA accumulators (VGPRs at 2 waves/SIMD): the hazard-safe conversion
-      const uint32_t lo = cvt_pk_bf16_cc(acc[j][t][0], acc[j][t][1]);
-      const uint32_t hi = cvt_pk_bf16_cc(acc[j][t][2], acc[j][t][3]);
+      const uint32_t lo = cvt_pk_bf16(acc[j][t][0], acc[j][t][1]);
+      const uint32_t hi = cvt_pk_bf16(acc[j][t][2], acc[j][t][3]);
       *reinterpret_cast<u32x2*>(zr + (int64_t)p * kCO) = u32x2{lo, hi};
       const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
                           __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
@@ -198,8 +194,8 @@ int mv_stem_partials(int N) {
 }
 
 void mv_stem_fwd(const void* x, const void* w, void* z, const float* shift, float* partial, int N,
-                 hipStream_t st, int grid) {
-  if (grid <= 0) grid = mv_stem_partials(N);
+                 hipStream_t st) {
+  const int grid = mv_stem_partials(N);
   hipLaunchKernelGGL(mv::stem::stem_fwd_kernel, dim3(grid), dim3(256), 0, st, (const __bf16*)x,
                      (const __bf16*)w, (__bf16*)z, shift, partial, N);
 }

@@ -1,6 +1,10 @@
 """Probe RCCL PreMulSum / ncclAvg on a 1-rank communicator: which elements of an
 odd-length buffer come back unscaled (round-3 finding: the last of 4097)."""
-import torch
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
 
 from mivod.parallel.transport import RcclTransport
 

@@ -1231,6 +1231,80 @@ def keras_static():
     print("OK", r)
 
 
+def keras_overlap():
+    """Keras DistributedOptimizer with the reduction overlapping the backward
+    (OverlappedGradientReducer: tensor hooks during autograd.grad -> pack -> comm
+    stream): several buckets, most launched INSIDE autograd.grad, one plan, same
+    weights as the static (after-backward) reducer, identical on every rank; then
+    the TF2-style example (config 2) on it: identical weights, averaged metrics,
+    and HOROVOD_TIMELINE collective phases per bucket."""
+    import json
+    import tempfile
+
+    import numpy as np
+
+    import mivod.keras as hk
+    import mivod.kerasfw as keras
+    tl = os.path.join(tempfile.mkdtemp(), "timeline.json")
+    os.environ["HOROVOD_TIMELINE"] = tl
+    os.environ["MIVOD_BUCKET_MB"] = "0.05"            # several buckets for a small model
+    os.environ["MIVOD_FIRST_BUCKET_MB"] = "0.01"
+    os.environ["MIVOD_LAST_BUCKET_MB"] = "0.01"
+    hvd.init()
+    r = hvd.rank()
+    rng = np.random.default_rng(100 + r)
+    xs = rng.standard_normal((6, 16, 32)).astype(np.float32)
+    ys = rng.integers(0, 4, (6, 16)).astype(np.int64)
+
+    def train(overlap):
+        os.environ["MIVOD_KERAS_OVERLAP"] = "1" if overlap else "0"
+        torch.manual_seed(0)
+        model = keras.Sequential([keras.layers.Dense(64, activation="relu"),
+                                  keras.layers.Dense(64, activation="relu"),
+                                  keras.layers.Dense(64, activation="relu"),
+                                  keras.layers.Dense(4)])
+        opt = hk.DistributedOptimizer(keras.optimizers.SGD(0.1, momentum=0.9))
+        model.compile(loss=keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=opt)
+        for x, y in zip(xs, ys):
+            model.train_on_batch(x, y)
+        flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+        return flat, opt
+
+    fo, opt_o = train(True)
+    fs, opt_s = train(False)
+    red = opt_o._hvd_overlap
+    assert red.plans == 1 and red.steps == len(xs), (red.plans, red.steps)
+    assert len(red.buckets) > 2, len(red.buckets)
+    assert red.launched_in_backward >= len(xs) * (len(red.buckets) - 1), \
+        (red.launched_in_backward, len(red.buckets))
+    assert opt_s._hvd_static.plans == 1 and opt_o._hvd_static.plans == 0
+    torch.testing.assert_close(fo.cpu(), fs.cpu(), rtol=1e-5, atol=1e-6)
+    allf = hvd.allgather(fo.unsqueeze(0))
+    assert torch.equal(allf[0], allf[1])
+    # config 2 (TF2-style example) on the overlapped path
+    os.environ["MIVOD_KERAS_OVERLAP"] = "1"
+    os.environ["MIVOD_BUCKET_MB"] = "1"
+    sys.path.insert(0, os.path.join(ROOT, "examples"))
+    os.environ["PS_MODEL_PATH"] = tempfile.mkdtemp()
+    from keras_mnist_tf2_style import main
+    hist, model = main(["--epochs", "2", "--steps", "10"])
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    allf = hvd.allgather(flat.unsqueeze(0))
+    assert torch.equal(allf[0], allf[1])
+    logs = hvd.allgather_object(hist.history)
+    assert logs[0]["loss"] == logs[1]["loss"], logs
+    assert model.optimizer._hvd_overlap.steps == 20
+    hvd.shutdown()
+    from mivod.utils import timeline as TL
+    TL.stop_timeline()
+    if r == 0:
+        ev = json.load(open(tl))
+        names = {e.get("name") for e in ev if e.get("ph") == "X"}
+        assert names & {"NCCL_ALLREDUCE", "RING_ALLREDUCE"}, names
+    print("OK", r)
+
+
 def gpu_rccl_watchdog():
     """The communicator watchdog: a collective that cannot complete within
     MIVOD_RCCL_TIMEOUT_S (here: queued behind a ~3 s spin kernel) makes the watchdog

@@ -143,16 +143,12 @@ def test_resnet_uses_conv3x3_bwd_fusion(cuda, monkeypatch):
 
     monkeypatch.setattr(nat, "conv3x3_bn_bwd", counted)
     monkeypatch.setenv("MIVOD_CONV3X3_DGRAD", "1")     # every width (default: <= 128)
-    monkeypatch.setenv("MIVOD_CONV1X1_BN_BWD", "1")    # opt-in (bench A/B neutral)
-    # the BN3 fold (ops.bn._Conv1x1BNFold) computes conv3's data gradient itself, so the
-    # 1x1 mode-1 reduce only runs with the fold off
-    monkeypatch.setenv("MIVOD_BN_FOLD", "0")
     torch.manual_seed(0)
     m = to_mixed_bf16(ResNet((2, 2, 2, 1), num_classes=10)).to(cuda)
     x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
     F.cross_entropy(m(x).float(), torch.randint(0, 10, (4,), device=cuda)).backward()
-    # 3x3: layer1.0, layer1.1, layer2.1, layer3.1 (x.0: stride 2); 1x1: every conv3 (BN2)
-    assert calls.count(3) == 4 and calls.count(1) == 7, calls
+    # 3x3: layer1.0, layer1.1, layer2.1, layer3.1 (x.0: stride 2)
+    assert calls.count(3) == 4, calls
 
 
 @pytest.mark.parametrize("n,c,k,h,w,s", [(2, 64, 64, 9, 7, 1), (3, 128, 128, 10, 10, 2),

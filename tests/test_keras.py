@@ -170,3 +170,9 @@ def test_keras_adam_matches_closed_form():
     lr_t = 0.1 * math.sqrt(1 - 0.999) / (1 - 0.9)
     expect = w0[0] - lr_t * mt / (vt.sqrt() + 1e-7)
     torch.testing.assert_close(lyr.weight.detach()[0], expect, rtol=1e-5, atol=1e-6)
+
+
+def test_keras_overlapped_reduction_two_ranks():
+    """The Keras gradient reduction overlapping autograd (forced on CPU: gloo)."""
+    from test_multiprocess import run_ranks
+    run_ranks("keras_overlap", 2, timeout=400)

@@ -24,3 +24,10 @@ def test_convnet_example_on_gpu(cuda, tmp_path, monkeypatch):
     from keras_mnist_convnet import main
     hist, score = main(["--epochs", "1", "--train-samples", "12800", "--no-export"])
     assert score[1] > 0.9, score
+
+
+def test_keras_overlap_two_ranks_one_gpu(cuda):
+    """Config 2 on the GPU with 2 real ranks sharing cuda:0 (gloo-gpu wire): the Keras
+    reduction overlaps autograd on the comm stream; identical weights, averaged logs."""
+    from test_multiprocess import run_ranks
+    run_ranks("keras_overlap", 2, timeout=300, extra_env={"MIVOD_TRANSPORT": "gloo-gpu"})

@@ -53,6 +53,8 @@ hvd.init()
 x = hvd.allreduce(torch.tensor([float(hvd.rank())]), op=hvd.Sum)
 print("rank", hvd.rank(), "size", hvd.size(), "local", hvd.local_rank(), "sum", float(x),
       "nccl_debug", os.environ.get("NCCL_DEBUG"))
+from mivod.common import basics
+print("store", basics.state().store_kind, flush=True)
 hvd.shutdown()
 ''' % ROOT
 
@@ -67,6 +69,53 @@ def test_launch_two_local_ranks(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "[0]<stdout>:rank 0 size 2 local 0 sum 1.0 nccl_debug INFO" in r.stdout, r.stdout
     assert "[1]<stdout>:rank 1 size 2 local 1 sum 1.0 nccl_debug INFO" in r.stdout, r.stdout
+    # the gloo world, rings and engine bootstrapped through the launcher's native store
+    assert "[0]<stdout>:store native" in r.stdout and "[1]<stdout>:store native" in r.stdout
+
+
+def test_native_rendezvous_store():
+    """csrc/engine/store.cc: blocking get, counters, wait/check, compare-set, delete,
+    timeouts — and as a torch.distributed.Store for a 3-rank gloo world."""
+    import threading
+    import time
+
+    from mivod.run.store import NativeStore, serve
+    srv = serve("127.0.0.1", 0)
+    try:
+        a = NativeStore("127.0.0.1", srv.port, 5.0)
+        b = NativeStore("127.0.0.1", srv.port, 5.0)
+        got = []
+        t = threading.Thread(target=lambda: got.append(b.get("k")))
+        t.start()
+        time.sleep(0.2)
+        a.set("k", "v1")                   # wakes the blocked get (server-side wait, no polling)
+        t.join(5)
+        assert got == [b"v1"]
+        assert a.add("n", 3) == 3 and b.add("n", 2) == 5
+        assert a.check(["k", "n"]) and not a.check(["missing"])
+        assert a.compare_set("k", b"v1", b"v2") == b"v2" and b.get("k") == b"v2"
+        assert a.compare_set("k", b"zz", b"v3") == b"v2"
+        assert a.num_keys() == 2 and a.delete_key("k") and not a.check(["k"])
+        import datetime
+        t0 = time.time()
+        try:
+            a.wait(["never"], datetime.timedelta(seconds=0.3))
+            raise AssertionError("wait did not time out")
+        except RuntimeError as e:
+            assert "timed out" in str(e) and time.time() - t0 < 3
+        script = ("import sys, torch, torch.distributed as dist; sys.path.insert(0, %r)\n"
+                  "from mivod.run.store import NativeStore\n"
+                  "r = int(sys.argv[1]); st = NativeStore('127.0.0.1', %d, 30.0)\n"
+                  "dist.init_process_group('gloo', store=st, rank=r, world_size=3)\n"
+                  "x = torch.tensor([r + 1.0]); dist.all_reduce(x); print('sum', x.item())\n"
+                  "dist.destroy_process_group()\n") % (ROOT, srv.port)
+        ps = [subprocess.Popen([sys.executable, "-c", script, str(r)], stdout=subprocess.PIPE,
+                               stderr=subprocess.STDOUT, text=True) for r in range(3)]
+        outs = [p.communicate(timeout=120)[0] for p in ps]
+        assert all(p.returncode == 0 and "sum 6.0" in o for p, o in zip(ps, outs)), outs
+        assert srv.requests > 10
+    finally:
+        srv.close()
 
 
 def test_launch_failure_kills_all(tmp_path):

@@ -1,0 +1,74 @@
+"""Convergence guard for the heavily fused ResNet-50.
+
+Twenty-plus fusions (BN folds, recompute, shortcut folds, stem kernels, fused pool+BN
+backward, MFMA convs / GEMMs) must train like the stock bf16 PyTorch path, not just
+match it on one forward/backward: 224x224 ResNet-50, batch 32, 200 SGD steps on a
+learnable synthetic set (10 classes, each a fixed smooth random image + noise), run
+once with every mivod fusion on and once on the stock path (MIOpen convs, eager
+BatchNorm) from identical weights and identical batches.  Both loss curves must fall
+and stay close window by window."""
+import copy
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+_KEYS = ("MIVOD_FUSED_BN", "MIVOD_CONV_DGRAD_FWD", "MIVOD_BN_TAP", "MIVOD_DOWNSAMPLE_TAP",
+         "MIVOD_CONV_BN_FUSE", "MIVOD_CONV_BN_BWD_FUSE", "MIVOD_CONV3X3", "MIVOD_WGRAD3X3",
+         "MIVOD_STEM_KERNEL")
+STEPS, BATCH, CLASSES, WIN = 200, 32, 10, 20
+
+
+def _data(dev):
+    g = torch.Generator(device=dev).manual_seed(7)
+    proto = torch.rand(CLASSES, 3, 14, 14, device=dev, generator=g)
+    proto = F.interpolate(proto, size=(224, 224), mode="bilinear", align_corners=False)
+    batches = []
+    for s in range(STEPS):
+        gs = torch.Generator(device=dev).manual_seed(1000 + s)
+        y = torch.randint(0, CLASSES, (BATCH,), device=dev, generator=gs)
+        x = proto[y] + 0.35 * torch.randn(BATCH, 3, 224, 224, device=dev, generator=gs)
+        batches.append((x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last), y))
+    return batches
+
+
+def _train(model, batches, fused, monkeypatch):
+    from mivod.optim import FusedSGD
+    for k in _KEYS:
+        monkeypatch.setenv(k, "1" if fused else "0")
+    monkeypatch.setenv("MIVOD_STEM_CHANNELS", "4" if fused else "3")
+    opt = FusedSGD(model.parameters(), lr=0.02, momentum=0.9, weight_decay=5e-5)
+    losses = []
+    for x, y in batches:
+        loss = F.cross_entropy(model(x).float(), y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        losses.append(loss.detach())
+    return [float(v) for v in torch.stack(losses).cpu()]
+
+
+def test_fused_resnet50_trains_like_stock(cuda, monkeypatch):
+    from mivod.models.resnet import resnet50, to_mixed_bf16
+    torch.manual_seed(0)
+    base = to_mixed_bf16(resnet50(num_classes=CLASSES)).to(cuda)
+    batches = _data(cuda)
+    lf = _train(copy.deepcopy(base), batches, True, monkeypatch)
+    ls = _train(copy.deepcopy(base), batches, False, monkeypatch)
+    for k in _KEYS + ("MIVOD_STEM_CHANNELS",):
+        os.environ.pop(k, None)
+    wf = [sum(lf[i:i + WIN]) / WIN for i in range(0, STEPS, WIN)]
+    ws = [sum(ls[i:i + WIN]) / WIN for i in range(0, STEPS, WIN)]
+    print("fused windows", [round(v, 3) for v in wf])
+    print("stock windows", [round(v, 3) for v in ws])
+    assert all(v == v for v in lf + ls), "non-finite loss"
+    # both learn: the last window is far below the first (chance level is ln 10 = 2.30)
+    assert wf[-1] < 0.35 * wf[0] and ws[-1] < 0.35 * ws[0], (wf, ws)
+    # and follow the same trajectory: every window within 25% (+0.05) of the other path,
+    # the final one within 5% of the first window's scale
+    for a, b in zip(wf, ws):
+        assert abs(a - b) <= 0.25 * max(a, b) + 0.05, (wf, ws)
+    assert abs(wf[-1] - ws[-1]) <= 0.05 * ws[0], (wf, ws)
