@@ -35,3 +35,12 @@ int64_t mv_wgrad1x1_workspace(int64_t M, int K, int C);
 bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
                  int K, int stride, hipStream_t st, bool dw_fp32 = false,
                  const void* dy2 = nullptr, int k1 = 0);
+
+// 64 -> 64 channel 3x3 / stride 1 "row patch" kernel (mv_conv64.hip): filter resident in
+// LDS, 8-row input patches staged once for all 9 taps.  W <= 62.  grid = persistent
+// workgroups (= the partial-row count when partial != null).  Same epilogues as
+// mv_conv3x3 (statistics / BN+ReLU backward reduce).
+bool mv_conv64_supported(int N, int H, int W, int C, int K, int ks, int stride);
+bool mv_conv64(const void* x, const void* w, void* y, int N, int H, int W, const float* shift,
+               float* partial, int grid, hipStream_t st, const void* bn_x = nullptr,
+               const float* bn_vec = nullptr);

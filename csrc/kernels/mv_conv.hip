@@ -401,6 +401,24 @@ bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, in
   using namespace mv::conv;
   if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2) || (ks != 1 && ks != 3))
     return false;
+  // 64 -> 64 channel 3x3 stride 1 (ResNet-50 layer1): the row-patch kernel (mv_conv64.hip)
+  static const bool c64 = [] {
+    const char* e = std::getenv("MIVOD_CONV64");
+    return !(e && e[0] == '0');
+  }();
+  if (c64 && mv_conv64_supported(N, H, W, C, K, ks, stride)) {
+    const int64_t M = (int64_t)N * H * W;
+    int grid = partial ? (int)mv_conv3x3_partials(M, K) : 0;
+    if (!partial) {
+      int dev = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          cus < 1)
+        cus = 256;
+      grid = cus;
+    }
+    return mv_conv64(x, w, y, N, H, W, shift, partial, grid, st, bn_x, bn_vec);
+  }
   Geo g;
   g.ks = ks;
   g.H = H;

@@ -19,7 +19,13 @@ def _cl(t):
 @pytest.mark.parametrize("n,c,h,w,k,s", [(2, 64, 9, 7, 64, 1), (3, 64, 16, 16, 128, 1),
                                          (2, 128, 12, 10, 128, 2), (1, 256, 7, 7, 256, 1),
                                          (2, 128, 15, 13, 64, 2), (4, 64, 56, 56, 64, 1),
-                                         (2, 512, 7, 7, 512, 1)])
+                                         (2, 512, 7, 7, 512, 1),
+                                         # 64 -> 64 stride 1 = the row-patch kernel
+                                         # (mv_conv64.hip): partial last row block, widest
+                                         # row (62), 1-pixel rows, and W = 63 (falls back)
+                                         (3, 64, 13, 9, 64, 1), (1, 64, 17, 62, 64, 1),
+                                         (2, 64, 5, 1, 64, 1), (1, 64, 8, 63, 64, 1),
+                                         (9, 64, 56, 56, 64, 1)])
 def test_conv3x3_matches_fp32(cuda, n, c, h, w, k, s):
     nat = _nat()
     g = torch.Generator(device=cuda).manual_seed(n * 1000 + c + h + k + s)
