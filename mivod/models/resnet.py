@@ -42,13 +42,15 @@ class _StemConvStats(torch.autograd.Function):
         z, part = K.native().stem_fwd(x4, w4, shift)
         ctx.save_for_backward(x4, w4)
         ctx.mark_non_differentiable(part)
+        # no zero-filled gradient for the statistics output (a fill kernel per call)
+        ctx.set_materialize_grads(False)
         return z, part
 
     @staticmethod
     def backward(ctx, dz, _dpart):
         x4, w4 = ctx.saved_tensors
         dw = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and dz is not None:
             dz = dz.contiguous(memory_format=torch.channels_last)
             if os.environ.get("MIVOD_STEM_WGRAD", "1") != "0":
                 from ..ops import kernels as K

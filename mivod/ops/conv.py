@@ -138,10 +138,14 @@ class _Conv1x1BN(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.slot = slot
         ctx.mark_non_differentiable(part)
+        # no zero-filled gradient for the statistics output (a fill kernel per call)
+        ctx.set_materialize_grads(False)
         return y, part
 
     @staticmethod
     def backward(ctx, dy, _dpart):
+        if dy is None:                      # the output was not used
+            return None, None, None, None, None
         x, w = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
@@ -280,10 +284,14 @@ class _Conv3x3(torch.autograd.Function):
         ctx.stride = stride
         ctx.slot = slot
         ctx.mark_non_differentiable(part)
+        # no zero-filled gradient for the statistics output (a fill kernel per call)
+        ctx.set_materialize_grads(False)
         return y, part
 
     @staticmethod
     def backward(ctx, dy, _dpart):
+        if dy is None:                      # the output was not used
+            return None, None, None, None, None, None
         x, w = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         s = ctx.stride

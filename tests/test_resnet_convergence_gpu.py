@@ -3,10 +3,11 @@
 Twenty-plus fusions (BN folds, recompute, shortcut folds, stem kernels, fused pool+BN
 backward, MFMA convs / GEMMs) must train like the stock bf16 PyTorch path, not just
 match it on one forward/backward: 224x224 ResNet-50, batch 32, 200 SGD steps on a
-learnable synthetic set (10 classes, each a fixed smooth random image + noise), run
-once with every mivod fusion on and once on the stock path (MIOpen convs, eager
-BatchNorm) from identical weights and identical batches.  Both loss curves must fall
-and stay close window by window."""
+learnable synthetic set (10 classes, each a fixed smooth random image + noise; SGD
+lr 0.01 with a 30-step linear warmup, zero-init residual BN), run once with every
+mivod fusion on and once on the stock path (MIOpen convs, eager BatchNorm) from
+identical weights and identical batches.  Both loss curves must fall from chance to
+< 10% of it and stay within 10% of each other window by window."""
 import copy
 import os
 
@@ -20,6 +21,7 @@ _KEYS = ("MIVOD_FUSED_BN", "MIVOD_CONV_DGRAD_FWD", "MIVOD_BN_TAP", "MIVOD_DOWNSA
          "MIVOD_CONV_BN_FUSE", "MIVOD_CONV_BN_BWD_FUSE", "MIVOD_CONV3X3", "MIVOD_WGRAD3X3",
          "MIVOD_STEM_KERNEL")
 STEPS, BATCH, CLASSES, WIN = 200, 32, 10, 20
+LR, WARMUP = 0.01, 30
 
 
 def _data(dev):
@@ -40,9 +42,11 @@ def _train(model, batches, fused, monkeypatch):
     for k in _KEYS:
         monkeypatch.setenv(k, "1" if fused else "0")
     monkeypatch.setenv("MIVOD_STEM_CHANNELS", "4" if fused else "3")
-    opt = FusedSGD(model.parameters(), lr=0.02, momentum=0.9, weight_decay=5e-5)
+    opt = FusedSGD(model.parameters(), lr=LR, momentum=0.9, weight_decay=5e-5)
     losses = []
-    for x, y in batches:
+    for i, (x, y) in enumerate(batches):
+        for grp in opt.param_groups:            # linear warmup (Goyal et al.)
+            grp["lr"] = LR * min(1.0, (i + 1) / WARMUP)
         loss = F.cross_entropy(model(x).float(), y)
         loss.backward()
         opt.step()
@@ -54,7 +58,7 @@ def _train(model, batches, fused, monkeypatch):
 def test_fused_resnet50_trains_like_stock(cuda, monkeypatch):
     from mivod.models.resnet import resnet50, to_mixed_bf16
     torch.manual_seed(0)
-    base = to_mixed_bf16(resnet50(num_classes=CLASSES)).to(cuda)
+    base = to_mixed_bf16(resnet50(num_classes=CLASSES, zero_init_residual=True)).to(cuda)
     batches = _data(cuda)
     lf = _train(copy.deepcopy(base), batches, True, monkeypatch)
     ls = _train(copy.deepcopy(base), batches, False, monkeypatch)
@@ -66,9 +70,10 @@ def test_fused_resnet50_trains_like_stock(cuda, monkeypatch):
     print("stock windows", [round(v, 3) for v in ws])
     assert all(v == v for v in lf + ls), "non-finite loss"
     # both learn: the last window is far below the first (chance level is ln 10 = 2.30)
-    assert wf[-1] < 0.35 * wf[0] and ws[-1] < 0.35 * ws[0], (wf, ws)
-    # and follow the same trajectory: every window within 25% (+0.05) of the other path,
-    # the final one within 5% of the first window's scale
+    assert wf[-1] < 0.1 * wf[0] and ws[-1] < 0.1 * ws[0], (wf, ws)
+    # and follow the same trajectory: every window within 10% (+0.01) of the stock path,
+    # the final one within 15% (+0.005).  (Round 3 on 1x MI355X: 2.323 -> 0.023 on both,
+    # the largest window gap 1.7%.)
     for a, b in zip(wf, ws):
-        assert abs(a - b) <= 0.25 * max(a, b) + 0.05, (wf, ws)
-    assert abs(wf[-1] - ws[-1]) <= 0.05 * ws[0], (wf, ws)
+        assert abs(a - b) <= 0.10 * b + 0.01, (wf, ws)
+    assert abs(wf[-1] - ws[-1]) <= 0.15 * ws[-1] + 0.005, (wf, ws)
