@@ -44,3 +44,9 @@ bool mv_conv64_supported(int N, int H, int W, int C, int K, int ks, int stride);
 bool mv_conv64(const void* x, const void* w, void* y, int N, int H, int W, const float* shift,
                float* partial, int grid, hipStream_t st, const void* bn_x = nullptr,
                const float* bn_vec = nullptr);
+// weight gradient of the 64 -> 64 3x3 / stride 1 conv on the row-patch scheme
+// (mv_conv64.hip): W % 4 == 0, W <= 56; writes fp32 partial [grid][9][64][64] rows for
+// mv_conv.hip's wgrad reduce
+bool mv_wgrad64_supported(int N, int H, int W, int C, int K, int stride);
+bool mv_wgrad64(const void* x, const void* dy, float* partial, int grid, int N, int H, int W,
+                hipStream_t st);

@@ -656,6 +656,28 @@ bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, in
   const int nkc = (K / 64) * (C / 64);
   const int64_t nchunks = (g.M + 31) / 32;
   const int ms = wgrad_msplit(nchunks, nkc);
+  static const bool w64 = [] {
+    const char* e = std::getenv("MIVOD_WGRAD64");
+    return !(e && e[0] == '0');
+  }();
+  if (w64 && mv_wgrad64_supported(N, H, W, C, K, stride)) {
+    // 64 -> 64 stride 1: the row-patch kernel (mv_conv64.hip), one persistent 136-KB-LDS
+    // workgroup per CU (<= ms partial rows, so the workspace above is large enough)
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          n < 1)
+        n = 256;
+      return n;
+    }();
+    const int grid = ms < cus ? ms : cus;
+    mv_wgrad64(x, dy, work, grid, N, H, W, st);
+    const int64_t n = (int64_t)9 * K * C;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       (const float*)work, (__bf16*)dw, K, C, grid);
+    return true;
+  }
   hipLaunchKernelGGL(wgrad3x3_kernel, dim3((unsigned)(nkc * ms)), dim3(WG_NT), 0, st,
                      (const __bf16*)x, (const __bf16*)dy, work, g, nkc, ms, nchunks);
   const int64_t n = (int64_t)9 * K * C;

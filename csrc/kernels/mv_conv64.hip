@@ -358,3 +358,198 @@ bool mv_conv64(const void* x, const void* w, void* y, int N, int H, int W, const
   }
   return true;
 }
+
+// ===========================================================================
+// Weight gradient of the same 64 -> 64 3x3 / stride 1 conv (ResNet-50 layer1), row patch:
+//   dW[k][tap][c] = sum_p dy[p][k] . X[pixel(p) + tap][c]
+// The general wgrad3x3 kernel stages, per 32-pixel chunk, the dy rows and NINE tap-shifted
+// X row tiles (every input row read 9x from L2).  Here a workgroup stages, per tile of
+// R = 8 output rows of one image, the dy rows (448 px x 64 k, 56 KB) and the (R + 2)-row
+// X patch (80 KB) once, and all 9 taps read their shifted pixels from the patch.  Both
+// MFMA operands are pixel(=reduction)-major and come from gfx950's transposed LDS reads
+// (ds_read_b64_tr_b16, 4 consecutive pixels per read: W % 4 == 0 keeps a group of 4 in
+// one image row, so a tap shift moves it to 4 consecutive patch pixels, and the padded
+// patch stride makes every tap a constant offset from tap (0, 0)).  8 waves:
+// wave w owns input-channel tile w & 3 (16 c) and output-channel tiles 2 (w >> 2) .. +1
+// for all 9 taps (18 accumulators), accumulated over the workgroup's tiles; fp32
+// partial [G][9][64][64] rows + mv_conv.hip's fixed-order wgrad reduce.
+// ===========================================================================
+namespace mv {
+namespace conv64 {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWThreads = 512;
+constexpr int kDyPix = kR * 56;                   // dy pixels staged per tile (W <= 56)
+constexpr int kWLoadsDy = kDyPix * 8 / kWThreads;   // 7
+constexpr int kWLoadsX = kPR;                       // 10 (one patch row per load)
+
+// dy tile: [448 px][64 k] bf16, 128-B rows; the 16-B chunk ch of pixel p is stored at
+// ch ^ dswz(p).  A transposed read's 32-lane half touches 8 consecutive pixels, 32 B each;
+// the 64 banks span 256 B, so the 4 even (odd) pixels must sit in distinct 32-B windows.
+__device__ __forceinline__ int dswz(int p) { return ((p >> 1) & 3) << 1; }
+// X patch: [10 rows][58 cols] pixels at a 160-B (80-element) stride, unswizzled: 8
+// consecutive pixels land on bank offsets 40 j mod 64 = {0, 40, 16, 56, 32, 8, 48, 24}
+// dwords, one 8-dword window each, and every tap shift (dr, dc) is the constant offset
+// (58 dr + dc) x 160 B from tap (0, 0).
+constexpr int kPS = 80;                    // patch pixel stride (elements)
+constexpr int kPC = 58;                    // patch columns (W + 2 <= 58)
+
+__device__ __forceinline__ bf16x8 tr8p(const __bf16* pa, const __bf16* pb) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pa);
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)pb);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 o = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+__global__ __launch_bounds__(kWThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void wgrad64_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ DY,
+                    float* __restrict__ partial, Geo64 g) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[kDyPix * kC + kPR * kPC * kPS];   // 147 KB
+  __bf16* ds = lds;
+  __bf16* ps = lds + kDyPix * kC;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ct = wv & 3, kh = wv >> 2;
+  const int gq = lane >> 4, cl = lane & 15;
+  const int W = g.W, H = g.H;
+  const int npix = kR * W;           // pixels per tile (W % 4 == 0, W <= 56)
+
+  // staging roles.  dy: pixel (tid >> 3) + 64 i, chunk tid & 7.  X: patch column tid >> 3
+  // (< 58) of patch row i, chunk tid & 7.
+  const int sch = tid & 7, spix = tid >> 3;
+  const bool colok = spix >= 1 && spix - 1 < W;
+  const int64_t xcoff = (int64_t)(spix - 1) * kC + sch * 8;
+  u32x4 pdy[kWLoadsDy], px[kWLoadsX];
+  auto gload = [&](int64_t t) {
+    const int n = (int)(t / g.hblocks), h0 = (int)(t - (int64_t)n * g.hblocks) * kR;
+    const __bf16* img = X + (int64_t)n * H * W * kC;
+#pragma unroll
+    for (int i = 0; i < kWLoadsX; ++i) {
+      const int ih = h0 + i - 1;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (colok && ih >= 0 && ih < H)
+        v = *reinterpret_cast<const u32x4*>(img + (int64_t)ih * W * kC + xcoff);
+      px[i] = v;
+    }
+    const __bf16* dimg = DY + (int64_t)n * H * W * kC;
+#pragma unroll
+    for (int i = 0; i < kWLoadsDy; ++i) {
+      const int p = spix + 64 * i;
+      const int r = p / W;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (p < npix && h0 + r < H)
+        v = *reinterpret_cast<const u32x4*>(dimg + ((int64_t)(h0 + r) * W + (p - r * W)) * kC +
+                                            sch * 8);
+      pdy[i] = v;
+    }
+  };
+
+  // MFMA k index -> pixel: lane group gq holds pixels 4 gq + {0..3} (first half of its 8)
+  // and 16 + 4 gq + {0..3} (second half) of the 32-pixel k step, so each 32-lane half of
+  // a transposed read touches 8 consecutive pixels.  dy read addresses (k step 0; the +32
+  // pixel step keeps dswz):
+  const __bf16* ads[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = 4 * gq + 16 * h + (cl >> 2), e = 16 * (2 * kh + u) + 4 * (cl & 3);
+      ads[u][h] = ds + r * 64 + (((e >> 3) ^ dswz(r)) << 3) + (e & 7);
+    }
+  const __bf16* pbase = ps + (cl >> 2) * kPS + 16 * ct + 4 * (cl & 3);
+  f32x4v acc[2][9];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) acc[u][tp] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  int64_t t = blockIdx.x;
+  if (t < g.tiles) gload(t);
+  for (; t < g.tiles; t += gridDim.x) {
+    __syncthreads();                      // previous tile's reads done
+    if (spix < kPC) {
+#pragma unroll
+      for (int i = 0; i < kWLoadsX; ++i)
+        *reinterpret_cast<u32x4*>(ps + (i * kPC + spix) * kPS + sch * 8) = px[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kWLoadsDy; ++i) {
+      const int p = spix + 64 * i;
+      *reinterpret_cast<u32x4*>(ds + p * 64 + ((sch ^ dswz(p)) << 3)) = pdy[i];
+    }
+    __syncthreads();
+    if (t + gridDim.x < g.tiles) gload(t + gridDim.x);
+    __builtin_amdgcn_sched_barrier(0);
+    // ceil(R W / 32) k steps of 32 pixels.  Pixels >= R W (and rows past H) are zero dy
+    // rows: they add nothing, and their patch index is clamped to 0 so every read stays
+    // inside the patch.  (row, col) of this lane's two pixel groups advance by 32 a step.
+    const int nks = (npix + 31) >> 5;
+    int ra = (4 * gq) / W, ca = 4 * gq - ra * W;
+    int rb = (4 * gq + 16) / W, cb = 4 * gq + 16 - rb * W;
+#pragma unroll 1
+    for (int ks = 0; ks < nks; ++ks) {
+      const int pa = ks * 32 + 4 * gq;
+      const int qa = pa < npix ? ra * kPC + ca : 0;
+      const int qb = pa + 16 < npix ? rb * kPC + cb : 0;
+      bf16x8 af[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) af[u] = tr8p(ads[u][0] + ks * 32 * 64, ads[u][1] + ks * 32 * 64);
+      const __bf16* ba = pbase + qa * kPS;
+      const __bf16* bb = pbase + qb * kPS;
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        const int off = ((tp / 3) * kPC + tp % 3) * kPS;
+        const bf16x8 bfr = tr8p(ba + off, bb + off);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[u][tp] = mfma(af[u], bfr, acc[u][tp]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      ca += 32;
+      while (ca >= W) {
+        ca -= W;
+        ++ra;
+      }
+      cb += 32;
+      while (cb >= W) {
+        cb -= W;
+        ++rb;
+      }
+    }
+  }
+  // partial[blockIdx][tap][k][c]; every block writes (zeros without tiles)
+  float* pp = partial + (int64_t)blockIdx.x * 9 * kC * kC;
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * (2 * kh + u) + 4 * gq + r, c = 16 * ct + cl;
+        pp[((int64_t)tp * kC + k) * kC + c] = acc[u][tp][r];
+      }
+}
+
+}  // namespace conv64
+}  // namespace mv
+
+bool mv_wgrad64_supported(int N, int H, int W, int C, int K, int stride) {
+  return N > 0 && C == 64 && K == 64 && stride == 1 && H >= 1 && W >= 4 && W % 4 == 0 &&
+         W <= 56 && (int64_t)H * W * 64 < (int64_t(1) << 31);
+}
+
+bool mv_wgrad64(const void* x, const void* dy, float* partial, int grid, int N, int H, int W,
+                hipStream_t st) {
+  using namespace mv::conv64;
+  if (!mv_wgrad64_supported(N, H, W, 64, 64, 1) || grid < 1) return false;
+  Geo64 g;
+  g.N = N;
+  g.H = H;
+  g.W = W;
+  g.hblocks = (H + kR - 1) / kR;
+  g.tiles = (int64_t)N * g.hblocks;
+  hipLaunchKernelGGL(wgrad64_kernel, dim3(grid), dim3(kWThreads), 0, st, (const __bf16*)x,
+                     (const __bf16*)dy, partial, g);
+  return true;
+}

@@ -158,7 +158,10 @@ def test_resnet_uses_conv3x3_bwd_fusion(cuda, monkeypatch):
 
 
 @pytest.mark.parametrize("n,c,k,h,w,s", [(2, 64, 64, 9, 7, 1), (3, 128, 128, 10, 10, 2),
-                                         (2, 64, 128, 8, 8, 1), (1, 256, 64, 7, 7, 1)])
+                                         (2, 64, 128, 8, 8, 1), (1, 256, 64, 7, 7, 1),
+                                         (2, 64, 64, 9, 8, 1), (1, 64, 64, 3, 4, 1),
+                                         (3, 64, 64, 13, 28, 1), (2, 64, 64, 56, 56, 1),
+                                         (5, 64, 64, 17, 52, 1)])
 def test_wgrad3x3_matches_fp32(cuda, n, c, k, h, w, s):
     nat = _nat()
     g = torch.Generator(device=cuda).manual_seed(n + c + k + h + s)
@@ -351,3 +354,23 @@ def test_stem_wgrad_kernel_matches_miopen(cuda, n):
                                               [3, 3], [1, 1], False, [0, 0], 1,
                                               [False, True, False])[1]
     torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 9, 8), (64, 56, 56), (3, 13, 28)])
+def test_wgrad64_matches_general_kernel(cuda, n, h, w):
+    """The 64 -> 64 row-patch weight gradient (mv_conv64.hip) vs the general wgrad3x3
+    kernel on the same inputs (MIVOD_WGRAD64 is read once per process, so the general
+    kernel is reached through a shape the row patch does not take: the same data with
+    one zero column appended, W + 1 not a multiple of 4)."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(n + h + w)
+    x = torch.randn(n, 64, h, w, device=cuda, generator=g).to(torch.bfloat16)
+    dy = torch.randn(n, 64, h, w, device=cuda, generator=g).to(torch.bfloat16)
+    dw = nat.wgrad3x3(_cl(x), _cl(dy), 1)
+    xp = F.pad(x, (0, 1)).contiguous()
+    dyp = F.pad(dy, (0, 1)).contiguous()
+    ref = nat.wgrad3x3(_cl(xp), _cl(dyp), 1)
+    # the padded column only adds x[.., w] = 0 / dy[.., w] = 0 products
+    assert torch.isfinite(dw.float()).all()
+    torch.testing.assert_close(dw.float(), ref.float(), rtol=1e-2,
+                               atol=1e-2 * float(ref.float().abs().max()))
