@@ -917,6 +917,58 @@ void gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> co,
              pp, cur_stream());
 }
 
+// the 256 x 256 kernel alone (A/B against gemm_nt's routing; plain C, no statistics)
+void gemm256_nt(at::Tensor a, at::Tensor b, at::Tensor c) {
+  for (const at::Tensor* t : {&a, &b, &c})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
+                    t->dim() == 2 && t->device() == a.device(),
+                "gemm256_nt: A, B, C must be contiguous 2-D bf16 tensors on one GPU");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm256_nt: shape mismatch");
+  TORCH_CHECK(mv_gemm256_supported(M, (int)N, (int)K),
+              "gemm256_nt: needs N % 256 == 0 and K % 64 == 0");
+  c10::DeviceGuard guard(a.device());
+  mv_gemm256_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, (int)N, (int)K, nullptr, nullptr,
+                cur_stream());
+}
+
+// strided 1x1 conv forward on the 256 x 256 kernel: y[Nb, Ho, Wo, N] (NHWC, returned as
+// channels_last NCHW) = conv1x1(x, w, stride ds), + BN statistics partials when shift is
+// given; None when the shape is not covered
+c10::optional<std::vector<at::Tensor>> conv1x1_strided_stats(at::Tensor x, at::Tensor w, int64_t ds,
+                                                             c10::optional<at::Tensor> shift) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv1x1_strided_stats: x must be a channels_last bf16 GPU tensor");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 1 &&
+                  w.size(3) == 1 && w.size(1) == x.size(1) && w.device() == x.device(),
+              "conv1x1_strided_stats: w must be a bf16 [N, C, 1, 1] filter");
+  TORCH_CHECK(ds >= 1, "conv1x1_strided_stats: stride >= 1");
+  const int64_t Nb = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), N = w.size(0);
+  const int64_t Ho = (H - 1) / ds + 1, Wo = (W - 1) / ds + 1, M = Nb * Ho * Wo;
+  if (!mv_gemm256_supported(M, (int)N, (int)C) || (shift.has_value() && N > 8192))
+    return c10::nullopt;
+  c10::DeviceGuard guard(x.device());
+  at::Tensor w2 = w.reshape({N, C}).contiguous();
+  at::Tensor y = at::empty({Nb, N, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor part;
+  float* pp = nullptr;
+  const float* sp = nullptr;
+  if (shift.has_value()) {
+    TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->numel() == N,
+                "conv1x1_strided_stats: shift must be fp32 [N]");
+    part = at::empty({mv_gemm256_partials(M), 2, N}, x.options().dtype(at::kFloat));
+    pp = part.data_ptr<float>();
+    sp = shift->data_ptr<float>();
+  }
+  if (!mv_gemm256_strided(x.data_ptr(), w2.data_ptr(), y.data_ptr(), (int)Nb, (int)H, (int)W,
+                          (int)C, (int)N, (int)ds, sp, pp, cur_stream()))
+    return c10::nullopt;
+  std::vector<at::Tensor> out{y};
+  if (pp) out.push_back(part);
+  return out;
+}
+
 int64_t gemm_fold_dx_partials(int64_t M, int64_t K1, int64_t K2) {
   return mv_gemm_fold_dx_partials(M, (int)K1, (int)K2);
 }
@@ -1592,4 +1644,8 @@ PYBIND11_MODULE(_mvk, m) {
         py::arg("x"), py::arg("dy"), py::arg("stride") = 1);
   m.def("conv3x3_partials", &conv3x3_partials, "partial rows of conv3x3's statistics epilogue");
   m.def("gemm_partials", &gemm_partials, "row tiles (statistics partial rows) of gemm_nt");
+  m.def("gemm256_nt", &gemm256_nt, "C = A . B^T on the 256x256 glds-pipelined kernel alone");
+  m.def("conv1x1_strided_stats", &conv1x1_strided_stats,
+        "[y, (partials)] of a strided 1x1 conv on the 256x256 kernel (+ BN statistics), or None",
+        py::arg("x"), py::arg("w"), py::arg("ds"), py::arg("shift") = py::none());
 }

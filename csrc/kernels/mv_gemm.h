@@ -56,3 +56,21 @@ bool mv_gemm_apply_dual_supported(int N, int K);
 bool mv_gemm_nt_apply_dual(const void* A, const void* B, const void* A2, const void* B2, void* Y,
                            int64_t M, int N, int K, const float* scale, const float* bias,
                            const float* rscale, const float* rbias, void* mask, hipStream_t st);
+
+// 256 x 256 tile, 8-wave glds pipeline (mv_gemm256.hip): N % 256 == 0, K % 64 == 0;
+// partial rows = mv_gemm256_partials(M).  mv_gemm_nt routes its tiled shapes here.
+bool mv_gemm256_supported(int64_t M, int N, int K);
+int64_t mv_gemm256_partials(int64_t M);
+bool mv_gemm256_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
+                   const float* shift, float* partial, hipStream_t st);
+// The strided 1x1 conv (stride ds) on the same kernel: X [Nb, H, W, K] NHWC, C [Nb * Ho *
+// Wo, N]; optional BN statistics (partial rows = mv_gemm256_partials(Nb * Ho * Wo)).
+bool mv_gemm256_strided(const void* X, const void* B, void* C, int Nb, int H, int W, int K, int N,
+                        int ds, const float* shift, float* partial, hipStream_t st);
+// D = [A1 | A2] . B^T + badd (A1 [M, K1], A2 [M, K2], B [N, K1 + K2]); with partial: the
+// BN fold's data-gradient epilogue (mv_gemm_fold_dx's, any N % 256 == 0): d = fma(xb,
+// scale, bias) > 0 ? bf16(D) : 0 is stored, partials [mv_gemm256_partials(M)][2][N] =
+// (sum d, sum d (xb - mean)); without: plain store
+bool mv_gemm256_dual(const void* A1, const void* A2, const void* B, const float* badd, void* D,
+                     int64_t M, int K1, int K2, int N, const void* xb, const float* mean,
+                     const float* scale, const float* bias, float* partial, hipStream_t st);

@@ -743,6 +743,15 @@ static bool launch_fold_dx(const __bf16* a, const __bf16* b, __bf16* d, int64_t 
 #define MV_STREAM_CASES(X) \
   X(64, 256) X(64, 128) X(64, 64) X(128, 256) X(128, 128) X(128, 64) X(256, 128) X(256, 64)
 
+// the 256 x 256 kernel (mv_gemm256.hip) for the tiled (K >= 512) shapes with N % 256 == 0
+static bool gemm256_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MIVOD_GEMM256");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // number of [2][N] statistics partial rows gemm_nt writes for this problem
 int64_t mv_gemm_partials(int64_t M, int N, int K) {
   int bn;
@@ -752,6 +761,7 @@ int64_t mv_gemm_partials(int64_t M, int N, int K) {
     MV_STREAM_CASES(MV_P)
 #undef MV_P
   }
+  if (gemm256_on() && mv_gemm256_supported(M, N, K)) return mv_gemm256_partials(M);
   const int bm = N % 128 == 0 ? 128 : 256;
   return (M + bm - 1) / bm;
 }
@@ -769,6 +779,7 @@ void mv_gemm_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
     MV_STREAM_CASES(MV_L)
 #undef MV_L
   }
+  if (gemm256_on() && mv_gemm256_nt(A, B, C, M, N, K, shift, partial, st)) return;
   if (N % 256 == 0)
     launch<128, 256, 2, 2>(a, b, c, M, N, K, shift, partial, st);
   else if (N % 128 == 0)
@@ -860,11 +871,17 @@ static bool fold_dx_dispatch(int K1, int K2, const __bf16* a, const __bf16* b, _
   return false;
 }
 
+// the 256 x 256 dual-source kernel for the fold data gradients the streaming kernel does
+// not cover (ResNet-50 layers 3-4: (K1, K2) = (1024, 256), (2048, 512))
+static bool fold_dx_g256(int64_t M, int K1, int K2) {
+  return gemm256_on() && K1 % 64 == 0 && mv_gemm256_supported(M, K2, K1 + K2) && 4 * K2 <= 8192;
+}
+
 int64_t mv_gemm_fold_dx_partials(int64_t M, int K1, int K2) {
   int64_t P = -1;
   mv::gemm::BwdEpi e{};
   if (!fold_dx_dispatch(K1, K2, nullptr, nullptr, nullptr, M, K2, e, nullptr, &P, nullptr))
-    return -1;
+    return fold_dx_g256(M, K1, K2) ? mv_gemm256_partials(M) : -1;
   return P;
 }
 
@@ -880,15 +897,24 @@ bool mv_gemm_fold_dx(const void* A1, const void* A2, const void* B, const float*
   e.badd = badd;
   e.ds = 1;
   int64_t P = 0;
-  return fold_dx_dispatch(K1, K2, (const __bf16*)A1, (const __bf16*)B, (__bf16*)D, M, K2, e,
-                          partial, &P, st);
+  if (fold_dx_dispatch(K1, K2, nullptr, nullptr, nullptr, M, K2, e, nullptr, &P, nullptr))
+    return fold_dx_dispatch(K1, K2, (const __bf16*)A1, (const __bf16*)B, (__bf16*)D, M, K2, e,
+                            partial, &P, st);
+  return fold_dx_g256(M, K1, K2) &&
+         mv_gemm256_dual(A1, A2, B, badd, D, M, K1, K2, K2, x, mean, scale, bias, partial, st);
 }
 
-bool mv_gemm_dual_supported(int K1, int K2) { return K1 == 256 && K2 == 64; }
+// (256, 64) on the streaming kernel; K2 % 256 == 0 on the 256 x 256 kernel
+bool mv_gemm_dual_supported(int K1, int K2) {
+  return (K1 == 256 && K2 == 64) || (gemm256_on() && K1 % 64 == 0 && K2 % 256 == 0);
+}
 
 bool mv_gemm_dual_bias(const void* A1, const void* A2, const void* B, const float* badd, void* D,
                        int64_t M, int K1, int K2, hipStream_t st) {
   if (!mv_gemm_dual_supported(K1, K2)) return false;
+  if (K2 % 256 == 0)
+    return mv_gemm256_dual(A1, A2, B, badd, D, M, K1, K2, K2, nullptr, nullptr, nullptr, nullptr,
+                           nullptr, st);
   mv::gemm::BwdEpi e{};
   e.a2 = (const __bf16*)A2;
   e.badd = badd;

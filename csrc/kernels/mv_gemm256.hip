@@ -1,0 +1,527 @@
+// 256 x 256 NT GEMM for the compute-bound 1x1 convolutions (ResNet-50 layers 3-4:
+// K = 256..2048, N = 256..2048), with the BN-statistics epilogue of mv_gemm.hip.
+//
+//   C[M, N] (bf16) = A[M, K] . B[N, K]^T, fp32 accumulation; N % 256 == 0, K % 64 == 0
+//
+// Why a second tiled kernel: mv_gemm.hip's 128 x 128 register-staged loop (two barriers
+// per 64-deep K step, ~1 block per SIMD pair) tops out near 550-620 TFLOP/s on these
+// shapes, below the vendor convolutions.  This one is built around the CDNA4 MFMA
+// pipeline instead:
+//   * 256 x 256 tile, 8 waves as 2 (M) x 4 (N), 128 x 64 outputs per wave (32 MFMA
+//     accumulators = 128 VGPRs): 128 FLOP per staged byte, one workgroup per CU.
+//   * Operands staged with global_load_lds (16 B per lane, LDS image lane-linear, the
+//     16-B chunk XOR swizzle applied to the SOURCE address and undone on the read).
+//     LDS = 2 K-tile buffers x 4 half-tiles (A rows of quadrant row 0 / 1, B columns
+//     of quadrant column 0 / 1) x 16 KB = 128 KB.
+//   * Each K tile runs as 4 phases, one per 64 x 32 output quadrant of the wave
+//     (16 MFMAs): the phase reads its operand half-tiles from LDS (A half 0 + B half 0,
+//     B half 1, A half 1, nothing), issues one half-tile of the NEXT K tile into the
+//     other buffer, and waits (counted vmcnt, never 0 in the steady state) for the
+//     half-tile the next phase reads.
+//   * Persistent (one workgroup per CU): one stream of K tiles runs over all of a
+//     workgroup's output tiles, so the next tile's first K tile is staged during the
+//     current tile's last one and its epilogue (short-K shapes: K = 256 is 4 K tiles).
+//   * The two wave groups (wm = 0 / 1, one wave of each per SIMD) run one barrier apart:
+//     while one group's phase is in its MFMA cluster (s_setprio 1), the other group is
+//     reading fragments and issuing loads, so each SIMD's matrix pipe always has a wave
+//     with MFMAs ready.  Reads of a staged half-tile always come one phase after the
+//     wait that retired it, which under the one-barrier stagger still orders every
+//     wave's DMA before any wave's read.
+// Output mapping as mv_gemm.hip: the filter tile is the MFMA A operand, so a lane's
+// 4 accumulators are 4 consecutive channels of one output row and the per-channel
+// statistics reduce over the 16 lanes of a lane group; C leaves as 16-byte stores after
+// a v_permlane16_swap exchange between n-tile pairs.
+#include "mv_common.h"
+#include "mv_gemm.h"
+
+#include <cstdlib>
+
+namespace mv {
+namespace g256 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int HALF = 128 * BK;            // elements per half-tile (16 KB)
+constexpr int BUF = 4 * HALF;             // one K tile: A0, A1, B0, B1
+
+__device__ __forceinline__ f32x4v mfma(const bf16x8& a, const bf16x8& b, const f32x4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int swz(int row, int ch) { return row * BK + ((ch ^ (row & 7)) << 3); }
+__device__ __forceinline__ float round_bf16(float x) { return (float)(__bf16)x; }
+__device__ __forceinline__ int remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+__device__ __forceinline__ void glds16(const void* src, __bf16* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0,
+                                   0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Kernel arguments.  A modes: 0 plain A[M, K]; 1 strided gather (a stride-ds 1x1 conv:
+// A is the [*, H, W, K] input, output row (n, ho, wo) reads input row (n, ho ds, wo ds));
+// 2 dual source (A columns [0, K1) from A [M, K1], [K1, K) from A2 [M, K - K1]).
+// Epilogues: 0 plain; 1 + BN statistics of the bf16 C around shift; 4 the BN fold's data
+// gradient (mv_gemm.hip EPI 4): C + badd, d = fma(xb, sc, bi) > 0 ? bf16 : 0 is stored,
+// partials (sum d, sum d (xb - mean)); 6 C + badd, plain store.
+struct Args {
+  const __bf16* A;
+  const __bf16* A2;
+  const __bf16* B;
+  __bf16* C;
+  int64_t M;
+  int N, K, K1, ntn;
+  int64_t ntiles;
+  int ds, H, W, Ho, Wo;
+  const float* shift;
+  float* partial;
+  const float* badd;
+  const __bf16* xb;
+  const float* mean;
+  const float* sc;
+  const float* bi;
+};
+
+template <int EPI>
+constexpr int nvec() { return EPI == 1 ? 1 : EPI == 4 ? 4 : EPI == 6 ? 1 : 0; }
+constexpr int kVecFloats = 8192;          // LDS for the per-channel epilogue vectors (32 KB)
+
+template <int EPI, int AMODE>
+__global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
+  constexpr int NV = nvec<EPI>();
+  constexpr bool STATS = EPI == 1 || EPI == 4;
+  constexpr bool BADD = EPI == 4 || EPI == 6;
+  // 2 K-tile buffers + the epilogue's per-channel vectors: ONE LDS object (a second one
+  // makes hipcc drain the in-flight LDS DMA before every fragment read)
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF + (NV ? 2 * kVecFloats : 0)];
+  float* vecs = reinterpret_cast<float*>(smem + 2 * BUF);     // [NV][N]
+  const int N = p.N;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int G = gridDim.x;
+  // persistent: workgroups of one XCD take consecutive tiles (the N tiles of an M block
+  // share its A rows through that XCD's L2)
+  int64_t tile = remap(blockIdx.x, G);
+  if (tile >= p.ntiles) return;
+
+  // ---- staging roles: glds instruction i (0, 1) of a half-tile lands at half row
+  // r = (2 w + i) * 8 + lane / 8, LDS chunk lane % 8, which holds source chunk
+  // (lane % 8) ^ (r & 7).  Half h of A = tile rows {128 q + 64 h + j}, of B = tile
+  // columns {64 q + 32 h + j}.  Byte offsets at K offset 0 (the host checks < 4 GB).
+  // (dual source: the A row index instead, both sources' offsets formed at issue)
+  uint32_t offa[2][2], offb[2][2];
+  const uint32_t scb = (uint32_t)(((lane & 7) ^ ((lane >> 3) & 7)) * 16);   // = sc * 16 bytes
+  const int KT = p.K / BK, KT1 = AMODE == 2 ? p.K1 / BK : KT;
+  auto set_src = [&](int64_t tl) {
+    const int64_t mt = tl / p.ntn;
+    const int nt = (int)(tl - mt * p.ntn);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (2 * w + i) * 8 + (lane >> 3);
+      const int sc = (lane & 7) ^ (r & 7);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int64_t row = mt * BM + (r >> 6) * 128 + h * 64 + (r & 63);
+        row = row < p.M ? row : p.M - 1;           // rows past M: a valid row, never stored
+        if constexpr (AMODE == 1) {
+          const int64_t hw = (int64_t)p.Ho * p.Wo;
+          const int64_t n = row / hw;
+          const int rem = (int)(row - n * hw);
+          const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+          row = (n * p.H + (int64_t)ho * p.ds) * p.W + (int64_t)wo * p.ds;
+        }
+        if constexpr (AMODE == 2) {
+          offa[h][i] = (uint32_t)row;
+        } else {
+          offa[h][i] = (uint32_t)((row * p.K + sc * 8) * 2);
+        }
+        const int col = nt * BN + (r >> 5) * 64 + h * 32 + (r & 31);
+        offb[h][i] = (uint32_t)(((int64_t)col * p.K + sc * 8) * 2);
+      }
+    }
+  };
+  auto issue = [&](int slot, int buf, int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const char* src;
+      if (slot >= 2) {
+        src = reinterpret_cast<const char*>(p.B) + offb[slot - 2][i] + kt * (BK * 2);
+      } else if (AMODE == 2) {
+        src = kt < KT1 ? reinterpret_cast<const char*>(p.A) + offa[slot][i] * (uint32_t)(p.K1 * 2) +
+                             scb + kt * (BK * 2)
+                       : reinterpret_cast<const char*>(p.A2) +
+                             offa[slot][i] * (uint32_t)((p.K - p.K1) * 2) + scb +
+                             (kt - KT1) * (BK * 2);
+      } else {
+        src = reinterpret_cast<const char*>(p.A) + offa[slot][i] + kt * (BK * 2);
+      }
+      glds16(src, smem + buf * BUF + slot * HALF + (2 * w + i) * 512);
+    }
+  };
+
+  f32x4v acc[4][8];                // [n tile][m tile]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bfr[2][2][2];   // A half frags [m tile][kk]; B [half][n tile][kk]
+  const int rl = lane & 15, g = lane >> 4;
+
+  auto read_a = [&](int buf, int h) {
+    const __bf16* base = smem + buf * BUF + h * HALF;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[b][kk] = *reinterpret_cast<const bf16x8*>(base + swz(wm * 64 + b * 16 + rl, kk * 4 + g));
+  };
+  auto read_b = [&](int buf, int h) {
+    const __bf16* base = smem + buf * BUF + (2 + h) * HALF;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bfr[h][a][kk] = *reinterpret_cast<const bf16x8*>(base + swz(wn * 32 + a * 16 + rl, kk * 4 + g));
+  };
+  auto mma = [&](int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[qn * 2 + a][qm * 4 + b] = mfma(bfr[qn][a][kk], af[b][kk], acc[qn * 2 + a][qm * 4 + b]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // C rows of this tile (+ the epilogue's statistics partial row (mt, wm)); no barrier:
+  // wave group 0 runs it while group 1 (one barrier behind) is still in its last MFMA
+  // phase, and the next tile's first K tile has already landed (waited before it: the
+  // counted waits never have to account for the epilogue's own loads and stores).
+  // 16-byte stores: v_permlane16_swap pairs n tiles (2q, 2q + 1) so that lane group g
+  // holds 8 consecutive channels of its row — g = 0 / 2: tile 2q columns 0-7 / 8-15,
+  // g = 1 / 3: tile 2q + 1 columns 0-7 / 8-15 (half the store instructions of the
+  // fragment layout's 8-byte stores, 64-B row segments instead of 32-B).
+  auto epilogue = [&](int64_t tl) {
+    const int64_t mt = tl / p.ntn;
+    const int n0 = (int)(tl - mt * p.ntn) * BN;
+    const int64_t m0 = mt * BM;
+    float s1[2][8], s2[2][8];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[q][j] = 0.f;
+        s2[q][j] = 0.f;
+      }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int64_t row = m0 + wm * 128 + b * 16 + rl;
+      const bool in = row < p.M;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        f32x4v u = acc[2 * q][b], v = acc[2 * q + 1][b];
+        if constexpr (BADD) {
+          const int cu = n0 + wn * 64 + 2 * q * 16 + 4 * g;
+          const f32x4v bu = *reinterpret_cast<const f32x4v*>(vecs + cu);
+          const f32x4v bv = *reinterpret_cast<const f32x4v*>(vecs + cu + 16);
+          u += bu;
+          v += bv;
+        }
+        uint32_t x0 = cvt_pk_bf16(u[0], u[1]), x1 = cvt_pk_bf16(u[2], u[3]);
+        uint32_t y0 = cvt_pk_bf16(v[0], v[1]), y1 = cvt_pk_bf16(v[2], v[3]);
+        const auto r0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        uint32_t o[4] = {r0[0], r1[0], r0[1], r1[1]};        // 8 consecutive channels
+        const int c0 = n0 + wn * 64 + q * 32 + (g & 1) * 16 + (g >> 1) * 8;
+        if constexpr (EPI == 1) {
+          if (in) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float f = (j & 1) ? __uint_as_float(o[j >> 1] & 0xffff0000u)
+                                      : __uint_as_float(o[j >> 1] << 16);
+              const float d = f - vecs[c0 + j];
+              s1[q][j] += d;
+              s2[q][j] += d * d;
+            }
+          }
+        }
+        if constexpr (EPI == 4) {
+          if (in) {
+            const uint4 xr = *reinterpret_cast<const uint4*>(p.xb + row * N + c0);
+            const uint32_t xw[4] = {xr.x, xr.y, xr.z, xr.w};
+            const float* mean = vecs + N;
+            const float* scv = vecs + 2 * N;
+            const float* biv = vecs + 3 * N;
+            float dv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float f = (j & 1) ? __uint_as_float(o[j >> 1] & 0xffff0000u)
+                                      : __uint_as_float(o[j >> 1] << 16);
+              const float xv = (j & 1) ? __uint_as_float(xw[j >> 1] & 0xffff0000u)
+                                       : __uint_as_float(xw[j >> 1] << 16);
+              const float d = __builtin_fmaf(xv, scv[c0 + j], biv[c0 + j]) > 0.f ? f : 0.f;
+              dv[j] = d;
+              s1[q][j] += d;
+              s2[q][j] += d * (xv - mean[c0 + j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = cvt_pk_bf16(dv[2 * j], dv[2 * j + 1]);
+          }
+        }
+        if (in) *reinterpret_cast<uint4*>(p.C + row * N + c0) = uint4{o[0], o[1], o[2], o[3]};
+      }
+    }
+    if constexpr (STATS) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s1[q][j] += __shfl_xor(s1[q][j], o, kWave);
+            s2[q][j] += __shfl_xor(s2[q][j], o, kWave);
+          }
+      if (rl == 0) {
+        float* pr = p.partial + (mt * 2 + wm) * 2 * N;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int c0 = n0 + wn * 64 + q * 32 + (g & 1) * 16 + (g >> 1) * 8;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            *reinterpret_cast<f32x4v*>(pr + c0 + 4 * h) =
+                f32x4v{s1[q][4 * h], s1[q][4 * h + 1], s1[q][4 * h + 2], s1[q][4 * h + 3]};
+            *reinterpret_cast<f32x4v*>(pr + N + c0 + 4 * h) =
+                f32x4v{s2[q][4 * h], s2[q][4 * h + 1], s2[q][4 * h + 2], s2[q][4 * h + 3]};
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // per-channel epilogue vectors -> LDS (EPI 1: shift; 4: badd, mean, sc, bi; 6: badd)
+  if constexpr (NV > 0) {
+    for (int c = tid; c < N; c += NT) {
+      if constexpr (EPI == 1) vecs[c] = p.shift ? p.shift[c] : 0.f;
+      if constexpr (BADD) vecs[c] = p.badd[c];
+      if constexpr (EPI == 4) {
+        vecs[N + c] = p.mean[c];
+        vecs[2 * N + c] = p.sc[c];
+        vecs[3 * N + c] = p.bi[c];
+      }
+    }
+  }
+  // prologue: this workgroup's first tile, K tile 0, in the consumption order A0, B0,
+  // B1, A1; A0 + B0 retired
+  set_src(tile);
+  issue(0, 0, 0);
+  issue(2, 0, 0);
+  issue(3, 0, 0);
+  issue(1, 0, 0);
+  wait_vm<4>();
+  barrier();
+  if (wm == 1) barrier();          // the one-barrier stagger of wave group 1
+
+  // one stream of K tiles over all of this workgroup's output tiles: the next tile's
+  // first K tile is staged during the current tile's last one (and its epilogue)
+  int kt = 0, buf = 0;
+  bool after = false;              // an epilogue ran since the last wait: nothing to retire
+  int64_t ntile = tile + G;
+  for (;;) {
+    const bool last_k = kt + 1 == KT;
+    const bool more = !last_k || ntile < p.ntiles;
+    const int nkt = last_k ? 0 : kt + 1;
+    const int nb = buf ^ 1;
+    if (last_k && more) set_src(ntile);
+    // Steady state: phase q issues one half-tile of the next K tile (A0', B0', B1', A1')
+    // and retires, by a counted wait, the half-tile phase q + 1 reads.  Before a tile's
+    // epilogue (last_k && more) the next tile's four half-tiles go out in phases 0-1 and
+    // are all retired in phase 3 — the epilogue's stores are then never inside a count.
+    // phase 0: quadrant (0, 0) — reads A0 + B0, retires B1
+    read_a(buf, 0);
+    read_b(buf, 0);
+    if (!more) {
+      wait_vm<2>();
+    } else if (last_k) {
+      issue(0, nb, nkt);
+      issue(2, nb, nkt);
+      wait_vm<4>();
+    } else {
+      issue(0, nb, nkt);
+      if (!after) wait_vm<4>();
+    }
+    barrier();
+    mma(0, 0);
+    barrier();
+    // phase 1: quadrant (0, 1) — reads B1, retires A1
+    read_b(buf, 1);
+    if (!more) {
+      wait_vm<0>();
+    } else if (last_k) {
+      issue(3, nb, nkt);
+      issue(1, nb, nkt);
+      wait_vm<8>();
+    } else {
+      issue(2, nb, nkt);
+      if (!after) wait_vm<4>();
+    }
+    barrier();
+    mma(0, 1);
+    barrier();
+    // phase 2: quadrant (1, 1) — reads A1
+    read_a(buf, 1);
+    if (more && !last_k) issue(3, nb, nkt);
+    barrier();
+    mma(1, 1);
+    barrier();
+    // phase 3: quadrant (1, 0) — no reads (B0 kept in registers); retires A0' + B0'
+    if (more) {
+      if (last_k) {
+        wait_vm<0>();
+      } else {
+        issue(1, nb, nkt);
+        wait_vm<4>();
+      }
+    }
+    barrier();
+    mma(1, 0);
+    barrier();
+    buf = nb;
+    after = last_k;
+    if (last_k) {
+      epilogue(tile);
+      if (!more) break;
+      tile = ntile;
+      ntile += G;
+      kt = 0;
+    } else {
+      ++kt;
+    }
+  }
+  if (wm == 0) barrier();          // close the stagger: equal barrier counts
+}
+
+}  // namespace g256
+}  // namespace mv
+
+static int g256_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+bool mv_gemm256_supported(int64_t M, int N, int K) {
+  return M > 0 && N % 256 == 0 && K % 64 == 0 && K >= 64 &&
+         (M + 255) / 256 * (N / 256) < (int64_t(1) << 31) && M * K * 2 < (int64_t(1) << 32) &&
+         (int64_t)N * K * 2 < (int64_t(1) << 32);
+}
+
+// two statistics rows (one per M wave group) per 256-row block
+int64_t mv_gemm256_partials(int64_t M) { return 2 * ((M + 255) / 256); }
+
+template <int EPI, int AMODE>
+static void g256_launch(mv::g256::Args a, hipStream_t st) {
+  using namespace mv::g256;
+  a.ntn = a.N / BN;
+  a.ntiles = (a.M + BM - 1) / BM * a.ntn;
+  const int cus = g256_cus();
+  const dim3 grid((unsigned)(a.ntiles < cus ? a.ntiles : cus));
+  hipLaunchKernelGGL((gemm256_kernel<EPI, AMODE>), grid, dim3(NT), 0, st, a);
+}
+
+bool mv_gemm256_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
+                   const float* shift, float* partial, hipStream_t st) {
+  using namespace mv::g256;
+  if (!mv_gemm256_supported(M, N, K) || (partial && N > kVecFloats)) return false;
+  Args a{};
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.shift = shift;
+  a.partial = partial;
+  if (partial) g256_launch<1, 0>(a, st);
+  else g256_launch<0, 0>(a, st);
+  return true;
+}
+
+bool mv_gemm256_strided(const void* X, const void* B, void* C, int Nb, int H, int W, int K, int N,
+                        int ds, const float* shift, float* partial, hipStream_t st) {
+  using namespace mv::g256;
+  const int Ho = (H - 1) / ds + 1, Wo = (W - 1) / ds + 1;
+  const int64_t M = (int64_t)Nb * Ho * Wo;
+  if (ds < 1 || !mv_gemm256_supported(M, N, K) || (partial && N > kVecFloats) ||
+      (int64_t)Nb * H * W * K * 2 >= (int64_t(1) << 32))
+    return false;
+  Args a{};
+  a.A = (const __bf16*)X;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.ds = ds;
+  a.H = H;
+  a.W = W;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.shift = shift;
+  a.partial = partial;
+  if (partial) g256_launch<1, 1>(a, st);
+  else g256_launch<0, 1>(a, st);
+  return true;
+}
+
+bool mv_gemm256_dual(const void* A1, const void* A2, const void* B, const float* badd, void* D,
+                     int64_t M, int K1, int K2, int N, const void* xb, const float* mean,
+                     const float* scale, const float* bias, float* partial, hipStream_t st) {
+  using namespace mv::g256;
+  const int K = K1 + K2;
+  if (K1 % 64 || K2 % 64 || !mv_gemm256_supported(M, N, K) || 4 * N > kVecFloats) return false;
+  Args a{};
+  a.A = (const __bf16*)A1;
+  a.A2 = (const __bf16*)A2;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)D;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.K1 = K1;
+  a.badd = badd;
+  a.xb = (const __bf16*)xb;
+  a.mean = mean;
+  a.sc = scale;
+  a.bi = bias;
+  a.partial = partial;
+  if (partial) g256_launch<4, 2>(a, st);
+  else g256_launch<6, 2>(a, st);
+  return true;
+}

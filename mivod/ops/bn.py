@@ -27,6 +27,8 @@ _RECOMPUTE = os.environ.get("MIVOD_BN_RECOMPUTE", "1") != "0"
 # 128 vs 256: 15,294 / 15,330 vs 15,304 / 15,282 img/s, level); blocks with a projection
 # shortcut keep it (its BN is applied in that epilogue)
 _RECOMPUTE_MAXK = int(os.environ.get("MIVOD_BN_RECOMPUTE_MAXK", "128"))
+# the 256 x 256 GEMM (mv_gemm256.hip) for the strided shortcut forward
+_GEMM256 = os.environ.get("MIVOD_GEMM256", "1") != "0"
 # MIVOD_BN_FOLD_DX=0: the fold's data gradient runs as two hipBLASLt GEMMs and BN2 runs its
 # own backward reduce pass, instead of mv_gemm's dual-source kernel with that reduce fused
 _FOLD_DX = os.environ.get("MIVOD_BN_FOLD_DX", "1") != "0"
@@ -551,8 +553,15 @@ class _Conv1x1BNFold(torch.autograd.Function):
                                 part_r)
                     zr_in = zrf.view(n, h, wd, cout).permute(0, 3, 1, 2)
                 else:
-                    zr_in = _cl(F.conv2d(residual, res_conv_w, None, s_r))
-                    part_r = None
+                    # strided shortcut conv + its BN statistics on the 256 x 256 GEMM
+                    # (rows gathered at the stride: no strided copy of the block input)
+                    r = (nat.conv1x1_strided_stats(residual, res_conv_w, s_r, rm_r)
+                         if _GEMM256 else None)
+                    if r is not None:
+                        zr_in, part_r = r[0], r[1]
+                    else:
+                        zr_in = _cl(F.conv2d(residual, res_conv_w, None, s_r))
+                        part_r = None
             else:
                 zr_in, dual = residual, None
             if part_r is not None:

@@ -174,12 +174,16 @@ class _Conv1x1BN(torch.autograd.Function):
 
 def stats_fusable(m: nn.Conv2d, x: torch.Tensor) -> bool:
     """1x1 / stride 1 convs whose forward mivod's GEMM runs at least as fast as
-    MIOpen (K = Cin in {64, 128, 256}, or Cin 512 -> Cout 128 on MI355X)."""
+    MIOpen: K = Cin in {64, 128, 256} (the streaming kernel), Cin 512 -> Cout 128, and
+    Cin >= 512 with Cout % 256 == 0 (the 256 x 256 kernel, mv_gemm256.hip:
+    scripts/micro_gemm256.py, 1024 -> 256 at 14x14 bs2048 270 us vs CK 342 us)."""
     if os.environ.get("MIVOD_CONV_BN_FUSE", "1") == "0" or not _eligible(m, x):
         return False
     cin, cout = m.in_channels, m.out_channels
+    big = (os.environ.get("MIVOD_GEMM256", "1") != "0" and cin >= 512 and cin % 64 == 0
+           and cout % 256 == 0)
     return (tuple(m.kernel_size) == (1, 1) and cout % 64 == 0
-            and (cin in (64, 128, 256) or (cin == 512 and cout == 128)))
+            and (cin in (64, 128, 256) or (cin == 512 and cout == 128) or big))
 
 
 def bwd_fusable(m: nn.Conv2d, x: torch.Tensor):

@@ -42,6 +42,35 @@ def test_gemm_nt_matches_fp32(cuda, M, K, N):
     assert torch.equal(c, c2)
 
 
+@pytest.mark.parametrize("M,K,N", [(256 * 700 + 37, 64, 256), (153637, 512, 512),
+                                   (300000, 256, 1024), (4096, 2048, 2048), (255, 128, 256)])
+def test_gemm256_persistent_matches_fp32(cuda, M, K, N):
+    """mv_gemm256.hip: several output tiles per persistent workgroup (the next tile's
+    first K tile staged during the previous epilogue), a ragged last row block, a single
+    K tile (K = 64); via gemm_nt (with statistics) where gemm_nt routes to it."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(M + K + N)
+    a = (torch.rand(M, K, device=cuda, generator=g) * 2 - 1).to(torch.bfloat16)
+    b = ((torch.rand(N, K, device=cuda, generator=g) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+    c = torch.full((M, N), float("nan"), device=cuda).to(torch.bfloat16)
+    nat.gemm256_nt(a, b, c)
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(c.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    c2 = torch.empty_like(c)
+    nat.gemm256_nt(a, b, c2)
+    assert torch.equal(c, c2)
+    if K >= 512:
+        shift = torch.randn(N, device=cuda, generator=g) * 0.1
+        part = torch.full((nat.gemm_partials(M, N, K), 2, N), float("nan"), device=cuda)
+        c3 = torch.empty_like(c)
+        nat.gemm_nt(a, b, c3, shift, part)
+        assert torch.equal(c3, c)
+        d = c.float() - shift
+        s = part.sum(0)
+        torch.testing.assert_close(s[0], d.sum(0), rtol=1e-4, atol=1e-2)
+        torch.testing.assert_close(s[1], (d * d).sum(0), rtol=1e-4, atol=1e-2)
+
+
 def test_gemm_nt_rejects_bad_shapes(cuda):
     nat = _nat()
     a = torch.zeros(8, 96, device=cuda, dtype=torch.bfloat16)
@@ -428,8 +457,8 @@ def test_resnet_bn_recompute_matches_materialised(cuda, monkeypatch):
         assert er <= 1.25 * em + 2e-2, (k, er, em)
 
 
-@pytest.mark.parametrize("K1,K2", [(256, 64), (512, 128)])
-@pytest.mark.parametrize("M", [1, 64 * 3 + 5, 4096 + 17])
+@pytest.mark.parametrize("K1,K2", [(256, 64), (512, 128), (1024, 256), (2048, 512)])
+@pytest.mark.parametrize("M", [1, 64 * 3 + 5, 4096 + 17, 70000])
 def test_gemm_fold_dx_matches_fp32(cuda, M, K1, K2):
     """Dual-source fold data gradient + BN2 ReLU-backward reduce epilogue vs fp32 math."""
     nat = _nat()
@@ -454,7 +483,7 @@ def test_gemm_fold_dx_matches_fp32(cuda, M, K1, K2):
     df = d.float()
     torch.testing.assert_close(s[0], df.sum(0), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(s[1], (df * (xb.float() - vec[0])).sum(0), rtol=1e-4, atol=1e-2)
-    assert nat.gemm_fold_dx_partials(M, 1024, 256) == -1      # not a covered shape
+    assert nat.gemm_fold_dx_partials(M, 1024, 128) == -1      # not a covered shape
 
 
 def test_resnet_fold_dx_matches_hipblaslt(cuda, monkeypatch):
@@ -556,7 +585,7 @@ def test_gemm_dual_bias_matches_fp32(cuda, M):
     """EPI 6: [a1 | a2] . b^T + badd with a plain bf16 store (the shortcut fold's dx0)."""
     nat = _nat()
     K1, K2 = 256, 64
-    assert nat.gemm_dual_supported(K1, K2) and not nat.gemm_dual_supported(512, 256)
+    assert nat.gemm_dual_supported(K1, K2) and not nat.gemm_dual_supported(512, 128)
     g = torch.Generator(device=cuda).manual_seed(M + 11)
     a1 = torch.randn(M, K1, device=cuda, generator=g).to(torch.bfloat16)
     a2 = torch.randn(M, K2, device=cuda, generator=g).to(torch.bfloat16)
@@ -727,3 +756,45 @@ def test_fold_math_kernels_match_eager(cuda, monkeypatch, cout, cin, colsum):
     for a, b, name in zip(out[True], out[False], ("dg", "db", "dw", "bcat", "badd")):
         torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2 * float(b.abs().max()),
                                    msg=name)
+
+
+@pytest.mark.parametrize("M,K1,K2", [(1, 512, 256), (64 * 3 + 5, 1024, 512), (70000, 2048, 1024)])
+def test_gemm_dual_bias_256(cuda, M, K1, K2):
+    """[a1 | a2] . b^T + badd on mv_gemm256.hip's dual-source mode (K2 % 256 == 0)."""
+    nat = _nat()
+    assert nat.gemm_dual_supported(K1, K2)
+    g = torch.Generator(device=cuda).manual_seed(M + K1)
+    a1 = torch.randn(M, K1, device=cuda, generator=g).to(torch.bfloat16)
+    a2 = torch.randn(M, K2, device=cuda, generator=g).to(torch.bfloat16)
+    b = (torch.randn(K2, K1 + K2, device=cuda, generator=g) / (K1 + K2) ** 0.5).to(torch.bfloat16)
+    badd = torch.randn(K2, device=cuda, generator=g) * 0.1
+    d = torch.full((M, K2), float("nan"), device=cuda).to(torch.bfloat16)
+    nat.gemm_dual_bias(a1, a2, b, badd, d)
+    ref = a1.float() @ b[:, :K1].float().t() + a2.float() @ b[:, K1:].float().t() + badd
+    torch.testing.assert_close(d.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("n,c,h,k,s", [(2, 256, 9, 512, 2), (8, 512, 28, 1024, 2),
+                                       (3, 1024, 14, 2048, 2), (2, 512, 7, 256, 1),
+                                       (1, 64, 5, 256, 3)])
+def test_conv1x1_strided_stats(cuda, n, c, h, k, s):
+    """Strided 1x1 conv (rows gathered at the stride) + BN statistics on mv_gemm256.hip."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(n + c + h + k)
+    x = torch.randn(n, c, h, h + 1, device=cuda, generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(k, c, 1, 1, device=cuda, generator=g) / c ** 0.5).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    shift = torch.randn(k, device=cuda, generator=g) * 0.1
+    r = nat.conv1x1_strided_stats(x, w, s, shift)
+    assert r is not None
+    y, part = r
+    ref = F.conv2d(x.float(), w.float(), None, s)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    d = (y.float() - shift.view(1, -1, 1, 1)).permute(1, 0, 2, 3).reshape(k, -1)
+    sp = part.sum(0)
+    torch.testing.assert_close(sp[0], d.sum(1), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(sp[1], (d * d).sum(1), rtol=1e-4, atol=1e-2)
+    y2 = nat.conv1x1_strided_stats(x, w, s)[0]
+    assert torch.equal(y, y2)
