@@ -23,6 +23,7 @@
 // accumulators are 4 consecutive output channels of one output pixel (8-byte stores).
 #include "mv_common.h"
 #include "mv_conv.h"
+#include "mv_gemm.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -895,7 +896,25 @@ int w1_msplit(int64_t nchunks, int ntiles, const W1Cfg& c) {
 }
 }  // namespace
 
+// stride-1 shapes with C, K (and the dual split k1) multiples of 256 run on the 256 x 256
+// pipeline (mv_gemm256.hip wgrad256_kernel)
+static bool w256_on(int64_t M, int C, int K, int k1, int stride) {
+  static const bool on = [] {
+    const char* e = std::getenv("MIVOD_WGRAD256");
+    return !(e && e[0] == '0');
+  }();
+  return on && stride == 1 && mv_wgrad256_supported(M, C, K, k1);
+}
+
 int64_t mv_wgrad1x1_workspace(int64_t M, int K, int C) {
+  if (w256_on(M, C, K, K, 1)) {
+    // the dual (k1 < K) call shares the shape test; size for whichever runs
+    const int64_t w256 = mv_wgrad256_splits(M, C, K) * (int64_t)K * C;
+    const W1Cfg c = w1_cfg(K, C);
+    const int nt = (K / (64 * c.wk * c.fk)) * (C / (64 * c.wc));
+    const int64_t old = (int64_t)w1_msplit((M + 32 * c.ws - 1) / (32 * c.ws), nt, c) * c.ws * K * C;
+    return w256 > old ? w256 : old;
+  }
   const W1Cfg c = w1_cfg(K, C);
   const int ntiles = (K / (64 * c.wk * c.fk)) * (C / (64 * c.wc));
   const int64_t nchunks = (M + 32 * c.ws - 1) / (32 * c.ws);
@@ -926,8 +945,13 @@ bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, in
   const W1Cfg c = w1_cfg(K, C);
   const int ntiles = (K / (64 * c.wk * c.fk)) * (C / (64 * c.wc));
   const int64_t nchunks = (g.M + 32 * c.ws - 1) / (32 * c.ws);
-  const int ms = w1_msplit(nchunks, ntiles, c);
+  int ms = w1_msplit(nchunks, ntiles, c);
   const dim3 grid((unsigned)(ntiles * ms)), blk((unsigned)(64 * c.wk * c.wc * c.ws));
+  bool w256 = false;
+  if (w256_on(g.M, C, K, g.k1, stride)) {
+    w256 = mv_wgrad256(x, dy, dy2, work, g.M, C, K, g.k1, st);
+    if (w256) ms = (int)mv_wgrad256_splits(g.M, C, K);
+  }
   const __bf16 *xp = (const __bf16*)x, *dp = (const __bf16*)dy;
 #define MV_W1F(WKV, WCV, WSV, NSV, FKV)                                                       \
   if (stride == 1)                                                                           \
@@ -937,7 +961,8 @@ bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, in
     hipLaunchKernelGGL((wgrad1x1_kernel<WKV, WCV, WSV, 2, NSV, FKV>), grid, blk, 0, st, xp, dp,  \
                        work, g, ntiles, ms, nchunks);
 #define MV_W1(WKV, WCV, WSV, NSV) MV_W1F(WKV, WCV, WSV, NSV, 1)
-  if (c.fk == 2) {
+  if (w256) {
+  } else if (c.fk == 2) {
     MV_W1F(2, 2, 1, 3, 2)
   } else if (c.wk == 4) {
     MV_W1(4, 2, 1, 3)
@@ -958,7 +983,7 @@ bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, in
   }
 #undef MV_W1
 #undef MV_W1F
-  const int P = ms * c.ws;
+  const int P = w256 ? ms : ms * c.ws;
   const int64_t E = (int64_t)K * C;
   const float* wk = work;
 #define MV_W1R(PSV, TO)                                                                        \

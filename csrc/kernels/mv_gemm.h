@@ -74,3 +74,9 @@ bool mv_gemm256_strided(const void* X, const void* B, void* C, int Nb, int H, in
 bool mv_gemm256_dual(const void* A1, const void* A2, const void* B, const float* badd, void* D,
                      int64_t M, int K1, int K2, int N, const void* xb, const float* mean,
                      const float* scale, const float* bias, float* partial, hipStream_t st);
+// 1x1 weight gradient on the 256 x 256 pipeline (stride 1): partial[S][K][C] fp32 with
+// S = mv_wgrad256_splits(M, C, K); DY channels [k1, K) from DY2 ([M, K - k1]) when k1 < K
+bool mv_wgrad256_supported(int64_t M, int C, int K, int k1);
+int64_t mv_wgrad256_splits(int64_t M, int C, int K);
+bool mv_wgrad256(const void* X, const void* DY, const void* DY2, float* partial, int64_t M, int C,
+                 int K, int k1, hipStream_t st);

@@ -752,9 +752,18 @@ static bool gemm256_on() {
   return on;
 }
 
+// shapes the 256 x 256 kernel takes before the streaming kernel (plain / statistics /
+// statistics-only): K = 256 -> N >= 1024 (ResNet-50 layer3 conv3, scripts/micro_gemm256.py:
+// 348 us vs 371 us at bs2048)
+static bool g256_first(int64_t M, int N, int K) {
+  return gemm256_on() && K == 256 && N % 256 == 0 && N >= 1024 && N <= 8192 &&
+         mv_gemm256_supported(M, N, K);
+}
+
 // number of [2][N] statistics partial rows gemm_nt writes for this problem
 int64_t mv_gemm_partials(int64_t M, int N, int K) {
   int bn;
+  if (g256_first(M, N, K)) return mv_gemm256_partials(M);
   if (stream_cfg(K, N, &bn)) {
 #define MV_P(KK, BB) \
     if (K == KK && bn == BB) return streams_for<KK, BB, 1>(M, N);
@@ -773,6 +782,7 @@ void mv_gemm_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
   const __bf16* b = (const __bf16*)B;
   __bf16* c = (__bf16*)C;
   int bn;
+  if (g256_first(M, N, K) && mv_gemm256_nt(A, B, C, M, N, K, shift, partial, st)) return;
   if (stream_cfg(K, N, &bn)) {
 #define MV_L(KK, BB) \
     if (K == KK && bn == BB) { launch_stream<KK, BB>(a, b, c, M, N, shift, partial, nullptr, st); return; }

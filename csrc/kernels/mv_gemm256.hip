@@ -286,7 +286,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
             for (int j = 0; j < 4; ++j) o[j] = cvt_pk_bf16(dv[2 * j], dv[2 * j + 1]);
           }
         }
-        if (in) *reinterpret_cast<uint4*>(p.C + row * N + c0) = uint4{o[0], o[1], o[2], o[3]};
+        if (in && (EPI != 1 || p.C))        // EPI 1 with C == null: statistics only
+          *reinterpret_cast<uint4*>(p.C + row * N + c0) = uint4{o[0], o[1], o[2], o[3]};
       }
     }
     if constexpr (STATS) {
@@ -422,6 +423,200 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   if (wm == 0) barrier();          // close the stagger: equal barrier counts
 }
 
+// ===========================================================================
+// 1x1 weight gradient on the same pipeline:  dW[k][c] = sum_m DY[m][k] . X[m][c]
+// (stride 1; C % 256 == 0, K % 256 == 0; DY's channels [k1, K) from DY2 when k1 < K —
+// the BN fold's [dz | x]^T x Gram pass).  One workgroup = one 256 (c) x 256 (k) output
+// tile over one contiguous pixel range (the reduction), fp32 partial [split][K][C] rows
+// reduced in a fixed order by mv_conv.hip's wgrad1x1 reduce.  The reduction dimension is
+// the pixel, the OUTER index of both NHWC operands, so the LDS images are pixel-major
+// [64 px][128 ch] half-tiles (256-B rows) and both MFMA operands come from gfx950's
+// transposed LDS reads (ds_read_b64_tr_b16: 4 consecutive pixels per read).  The 16-B
+// chunk XOR (row & 3) | (row >> 3 & 1) << 2 (in 32-B pairs) spreads the rows one
+// 32-lane half reads ({r..r+3, r+8..r+11}) over the 8 distinct 32-B bank windows.
+// MFMA A = X^T (c rows), B = DY (k columns): a lane's accumulators are 4 consecutive
+// c of one k — 16-byte partial stores.  Waves 2 (c) x 4 (k), 128 c x 64 k per wave, the
+// 4-phase / one-barrier-stagger K loop of gemm256_kernel.
+// ===========================================================================
+__device__ __attribute__((aligned(16))) uint32_t g_w256_zero[64];     // zero page (rows >= M)
+
+struct WArgs {
+  const __bf16* X;
+  const __bf16* DY;
+  const __bf16* DY2;
+  float* partial;
+  int64_t M;
+  int C, K, k1, ntc, ntiles, ms;
+  int64_t per;                  // 64-pixel chunks per split
+};
+
+__device__ __forceinline__ int wf(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
+
+// The transposed reads are inline asm: hipcc treats the ds_read_tr builtin as aliasing
+// the in-flight LDS DMA and drains vmcnt(0) before every one (the whole prefetch).  The
+// consumer waits lgkmcnt(0) itself (mma_wait), ahead of the MFMAs.
+typedef short s16x4w __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s16x4w tr_asm(const __bf16* p) {
+  s16x4w v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1"
+               : "=v"(v)
+               : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p));
+  return v;
+}
+__device__ __forceinline__ bf16x8 trp(const __bf16* pa, const __bf16* pb) {
+  const s16x4w a = tr_asm(pa);
+  const s16x4w b = tr_asm(pb);
+  typedef short s16x8w __attribute__((ext_vector_type(8)));
+  const s16x8w o = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+__global__ __launch_bounds__(NT, 1) void wgrad256_kernel(WArgs p) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = w >> 2, wk = w & 3;
+  // workgroups of one XCD share a pixel split (consecutive ids: same rows, other tiles)
+  const int t = remap(blockIdx.x, gridDim.x);
+  const int split = t / p.ntiles, tl = t - split * p.ntiles;
+  const int c0 = (tl % p.ntc) * 256, k0 = (tl / p.ntc) * 256;
+  const int64_t mb = (int64_t)split * p.per * BK;
+  int64_t me = mb + p.per * BK;
+  me = me < p.M ? me : p.M;
+  const int KT = me > mb ? (int)((me - mb + BK - 1) / BK) : 0;
+
+  // staging: glds instruction i of a half-tile = pixel rows (2 w + i) * 4 + lane / 16 of
+  // the 64-pixel chunk, LDS chunk lane % 16, holding logical chunk (lane % 16) ^ wf(row)
+  const __bf16* srcb[4];         // per slot: channel base of instruction i = 0 / 1 (i adds 0)
+  int choff[4][2];
+  const bool dual = p.k1 < p.K && k0 >= p.k1;
+  const __bf16* dyb = dual ? p.DY2 : p.DY;
+  const int ldy = dual ? p.K - p.k1 : p.k1;
+  const int kb = dual ? k0 - p.k1 : k0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (2 * w + i) * 4 + (lane >> 4);
+    const int lc = (lane & 15) ^ wf(r);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      choff[h][i] = c0 + 128 * (lc >> 3) + 64 * h + 8 * (lc & 7);          // X half h
+      choff[2 + h][i] = kb + 64 * (lc >> 2) + 32 * h + 8 * (lc & 3);       // DY half h
+    }
+  }
+  srcb[0] = srcb[1] = p.X;
+  srcb[2] = srcb[3] = dyb;
+  auto issue = [&](int slot, int buf, int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t row = mb + (int64_t)kt * BK + (2 * w + i) * 4 + (lane >> 4);
+      const int ld = slot < 2 ? p.C : ldy;
+      const void* src = row < me ? (const void*)(srcb[slot] + row * ld + choff[slot][i])
+                                 : (const void*)(g_w256_zero + (lane & 15) * 4);
+      glds16(src, smem + buf * BUF + slot * HALF + (2 * w + i) * 512);
+    }
+  };
+
+  f32x4v acc[4][8];                // [k tile][c tile]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bfr[2][2][2];
+  const int rl = lane & 15, g = lane >> 4;
+  // transposed-read element offset of (pixel row r, half-local channel e)
+  auto toff = [&](int r, int e) { return r * 128 + (((e >> 3) ^ wf(r)) << 3) + (e & 7); };
+  auto read_a = [&](int buf, int h) {          // X^T fragments: c tiles of half h
+    const __bf16* base = smem + buf * BUF + h * HALF;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int r = 32 * kk + 8 * g + (rl >> 2), e = 64 * wc + 16 * b + 4 * (rl & 3);
+        af[b][kk] = trp(base + toff(r, e), base + toff(r + 4, e));
+      }
+  };
+  auto read_b = [&](int buf, int h) {          // DY fragments: k tiles of half h
+    const __bf16* base = smem + buf * BUF + (2 + h) * HALF;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int r = 32 * kk + 8 * g + (rl >> 2), e = 32 * wk + 16 * a + 4 * (rl & 3);
+        bfr[h][a][kk] = trp(base + toff(r, e), base + toff(r + 4, e));
+      }
+  };
+  auto mma = [&](int qc, int qk) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // this phase's asm reads
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[qk * 2 + a][qc * 4 + b] = mfma(af[b][kk], bfr[qk][a][kk], acc[qk * 2 + a][qc * 4 + b]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if (KT > 0) {
+    issue(0, 0, 0);
+    issue(2, 0, 0);
+    issue(3, 0, 0);
+    issue(1, 0, 0);
+    wait_vm<4>();
+    barrier();
+    if (wc == 1) barrier();
+    for (int kt = 0; kt < KT; ++kt) {
+      const int buf = kt & 1, nb = buf ^ 1;
+      const bool more = kt + 1 < KT;
+      read_a(buf, 0);
+      read_b(buf, 0);
+      if (more) {
+        issue(0, nb, kt + 1);
+        wait_vm<4>();
+      } else {
+        wait_vm<2>();
+      }
+      barrier();
+      mma(0, 0);
+      barrier();
+      read_b(buf, 1);
+      if (more) {
+        issue(2, nb, kt + 1);
+        wait_vm<4>();
+      } else {
+        wait_vm<0>();
+      }
+      barrier();
+      mma(0, 1);
+      barrier();
+      read_a(buf, 1);
+      if (more) issue(3, nb, kt + 1);
+      barrier();
+      mma(1, 1);
+      barrier();
+      if (more) {
+        issue(1, nb, kt + 1);
+        wait_vm<4>();
+      }
+      barrier();
+      mma(1, 0);
+      barrier();
+    }
+    if (wc == 0) barrier();
+  }
+  // partial[split][k][c .. c + 3] (zeros for an empty split)
+  float* pp = p.partial + (int64_t)split * p.K * p.C;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int k = k0 + 64 * wk + 16 * a + rl, c = c0 + 128 * wc + 16 * b + 4 * g;
+      *reinterpret_cast<f32x4v*>(pp + (int64_t)k * p.C + c) = acc[a][b];
+    }
+}
+
 }  // namespace g256
 }  // namespace mv
 
@@ -458,7 +653,8 @@ static void g256_launch(mv::g256::Args a, hipStream_t st) {
 bool mv_gemm256_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
                    const float* shift, float* partial, hipStream_t st) {
   using namespace mv::g256;
-  if (!mv_gemm256_supported(M, N, K) || (partial && N > kVecFloats)) return false;
+  if (!mv_gemm256_supported(M, N, K) || (partial && N > kVecFloats) || (!C && !partial))
+    return false;
   Args a{};
   a.A = (const __bf16*)A;
   a.B = (const __bf16*)B;
@@ -523,5 +719,48 @@ bool mv_gemm256_dual(const void* A1, const void* A2, const void* B, const float*
   a.partial = partial;
   if (partial) g256_launch<4, 2>(a, st);
   else g256_launch<6, 2>(a, st);
+  return true;
+}
+
+// ---------------------------------------------------------------- 1x1 weight gradient
+bool mv_wgrad256_supported(int64_t M, int C, int K, int k1) {
+  return M > 0 && C % 256 == 0 && K % 256 == 0 && k1 > 0 && k1 <= K && k1 % 256 == 0 &&
+         M < (int64_t(1) << 31);
+}
+
+static void w256_split(int64_t M, int C, int K, int* ms, int64_t* per) {
+  const int ntiles = (C / 256) * (K / 256);
+  const int64_t chunks = (M + 63) / 64;
+  int m = g256_cus() / ntiles;
+  if (m < 1) m = 1;
+  if (m > chunks) m = (int)chunks;
+  *per = (chunks + m - 1) / m;
+  *ms = (int)((chunks + *per - 1) / *per);
+}
+
+int64_t mv_wgrad256_splits(int64_t M, int C, int K) {
+  int ms;
+  int64_t per;
+  w256_split(M, C, K, &ms, &per);
+  return ms;
+}
+
+bool mv_wgrad256(const void* X, const void* DY, const void* DY2, float* partial, int64_t M, int C,
+                 int K, int k1, hipStream_t st) {
+  using namespace mv::g256;
+  if (!mv_wgrad256_supported(M, C, K, k1) || (k1 < K && !DY2)) return false;
+  WArgs a{};
+  a.X = (const __bf16*)X;
+  a.DY = (const __bf16*)DY;
+  a.DY2 = (const __bf16*)DY2;
+  a.partial = partial;
+  a.M = M;
+  a.C = C;
+  a.K = K;
+  a.k1 = k1;
+  a.ntc = C / 256;
+  a.ntiles = (C / 256) * (K / 256);
+  w256_split(M, C, K, &a.ms, &a.per);
+  hipLaunchKernelGGL(wgrad256_kernel, dim3((unsigned)(a.ntiles * a.ms)), dim3(NT), 0, st, a);
   return true;
 }

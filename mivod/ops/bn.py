@@ -184,9 +184,9 @@ class _DownsampleTapConv(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dw = None
         if ctx.needs_input_grad[0]:
-            wt = w.transpose(0, 1).contiguous(memory_format=torch.channels_last)
+            from .conv import dgrad1x1
             assert ctx.slot.grad is None, "a tapped output has one shortcut consumer"
-            ctx.slot.grad = F.conv2d(dy, wt).contiguous(memory_format=torch.channels_last)
+            ctx.slot.grad = dgrad1x1(dy, w).contiguous(memory_format=torch.channels_last)
             ctx.slot.stride = ctx.s
             ctx.slot.full_shape = x.shape
         if ctx.needs_input_grad[1]:
@@ -623,7 +623,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        from .conv import _transposed_filter, wgrad1x1
+        from .conv import dgrad1x1, wgrad1x1
         x, w, z, keep, vec, weight, vec_r, res_w, zr, res_conv_w = ctx.saved_tensors
         slot = ctx.slot
         slot.bn = None
@@ -684,7 +684,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
                 dy2, s2 = slot.take_strided()
                 dlz, dg, db, dz = nat.bn_bwd(3, dy, z, keep, vec, weight, True, dy2, s2)
             if need_x:
-                dx = F.conv2d(dlz, _transposed_filter(w))
+                dx = dgrad1x1(dlz, w)
             if need_w:
                 dw = wgrad1x1(dlz, x, w)
         dres = dz if ctx.needs_input_grad[8] else None

@@ -44,6 +44,24 @@ def _transposed_filter(w: torch.Tensor) -> torch.Tensor:
     return wt.contiguous(memory_format=torch.channels_last)
 
 
+def dgrad1x1(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """Input gradient of a stride-1 1x1 conv, dX = dY . W as an NHWC GEMM: mivod's
+    256 x 256 kernel (mv_gemm256.hip) when Cin % 256 == 0 and Cout >= 256, else the
+    forward conv with the transposed filter (CK)."""
+    cout, cin = w.shape[0], w.shape[1]
+    if (os.environ.get("MIVOD_GEMM256", "1") != "0" and cin % 256 == 0 and cout % 64 == 0
+            and cout >= 256 and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and dy.is_contiguous(memory_format=torch.channels_last)):
+        from . import kernels as K
+        n, _, h, wd = dy.shape
+        m = n * h * wd
+        dx = torch.empty(m, cin, dtype=dy.dtype, device=dy.device)
+        K.native().gemm_nt(dy.permute(0, 2, 3, 1).reshape(m, cout),
+                           w.reshape(cout, cin).t().contiguous(), dx, None, None)
+        return dx.view(n, h, wd, cin).permute(0, 3, 1, 2)
+    return F.conv2d(dy, _transposed_filter(w))
+
+
 def _wgrad1x1_on_mivod(cin: int, cout: int) -> bool:
     """mivod's 1x1 weight-gradient kernel (csrc/kernels/mv_conv.hip wgrad1x1_kernel) vs
     MIOpen's backward-weights solver on the ResNet-50 bs2048 shapes (scripts/
@@ -78,7 +96,8 @@ class _ConvDgradFwd(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = F.conv2d(dy, _transposed_filter(w), None, 1, ctx.pad)
+            dx = (dgrad1x1(dy, w) if w.shape[2] == 1 and w.shape[3] == 1
+                  else F.conv2d(dy, _transposed_filter(w), None, 1, ctx.pad))
         if ctx.needs_input_grad[1]:
             if w.shape[2] == 1 and w.shape[3] == 1:
                 dw = wgrad1x1(dy, x, w)
@@ -166,7 +185,7 @@ class _Conv1x1BN(torch.autograd.Function):
                     h, wd)
                 slot.pending = (dz, part)
             else:
-                dx = F.conv2d(dy, _transposed_filter(w))
+                dx = dgrad1x1(dy, w)
         if ctx.needs_input_grad[1]:
             dw = wgrad1x1(dy, x, w)
         return dx, dw, None, None, None

@@ -179,7 +179,9 @@ def test_wgrad3x3_matches_fp32(cuda, n, c, k, h, w, s):
 @pytest.mark.parametrize("n,c,k,h,w,s", [(2, 128, 256, 9, 7, 1), (3, 256, 128, 10, 10, 2),
                                          (2, 64, 256, 8, 9, 1), (2, 256, 64, 7, 7, 1),
                                          (3, 64, 64, 11, 5, 1), (2, 512, 1024, 7, 7, 2),
-                                         (1, 64, 128, 3, 3, 2)])
+                                         (1, 64, 128, 3, 3, 2), (3, 512, 256, 9, 9, 1),
+                                         (2, 256, 512, 13, 13, 1), (64, 256, 256, 28, 28, 1),
+                                         (1, 256, 256, 1, 1, 1)])
 def test_wgrad1x1_matches_fp32(cuda, n, c, k, h, w, s):
     """All four tile layouts (128x128, 128x64 / 64x128 with 2 m slices, 64x64 with 4),
     stride 1 and 2 (odd sizes), m tails that are not multiples of the stage rows."""
@@ -322,7 +324,7 @@ def test_resnet_stem_kernel_path(cuda, monkeypatch):
 
 
 @pytest.mark.parametrize("n,c,k,h,s", [(2, 64, 256, 9, 1), (2, 128, 512, 8, 1), (1, 256, 512, 10, 2),
-                                       (1, 256, 1024, 7, 1)])
+                                       (1, 256, 1024, 7, 1), (40, 512, 2048, 7, 1)])
 def test_wgrad1x1_dual_dy(cuda, n, c, k, h, s):
     """wgrad1x1 with a second dy stream: [dy | dy2]^T . x == the two products stacked."""
     nat = _nat()

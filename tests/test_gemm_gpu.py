@@ -59,7 +59,7 @@ def test_gemm256_persistent_matches_fp32(cuda, M, K, N):
     c2 = torch.empty_like(c)
     nat.gemm256_nt(a, b, c2)
     assert torch.equal(c, c2)
-    if K >= 512:
+    if K >= 512 or (K == 256 and N >= 1024):
         shift = torch.randn(N, device=cuda, generator=g) * 0.1
         part = torch.full((nat.gemm_partials(M, N, K), 2, N), float("nan"), device=cuda)
         c3 = torch.empty_like(c)
@@ -69,6 +69,10 @@ def test_gemm256_persistent_matches_fp32(cuda, M, K, N):
         s = part.sum(0)
         torch.testing.assert_close(s[0], d.sum(0), rtol=1e-4, atol=1e-2)
         torch.testing.assert_close(s[1], (d * d).sum(0), rtol=1e-4, atol=1e-2)
+        if K == 256:                 # statistics only (C = None): the same partials
+            part2 = torch.full_like(part, float("nan"))
+            nat.gemm_nt(a, b, None, shift, part2)
+            assert torch.equal(part2, part)
 
 
 def test_gemm_nt_rejects_bad_shapes(cuda):
