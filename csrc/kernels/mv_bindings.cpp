@@ -957,7 +957,7 @@ c10::optional<std::vector<at::Tensor>> conv1x1_strided_stats(at::Tensor x, at::T
   if (shift.has_value()) {
     TORCH_CHECK(shift->is_cuda() && shift->scalar_type() == at::kFloat && shift->numel() == N,
                 "conv1x1_strided_stats: shift must be fp32 [N]");
-    part = at::empty({mv_gemm256_partials(M), 2, N}, x.options().dtype(at::kFloat));
+    part = at::empty({mv_gemm256_partials(M, (int)N), 2, N}, x.options().dtype(at::kFloat));
     pp = part.data_ptr<float>();
     sp = shift->data_ptr<float>();
   }

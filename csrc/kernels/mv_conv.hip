@@ -383,8 +383,19 @@ static int64_t streams_for(int64_t ntm, int ntn) {
 
 static int conv_bn_of(int K) { return K % 128 == 0 ? 128 : 64; }
 
+// Cout % 256 == 0 (ResNet-50 layers 3-4): the 256 x 256 glds pipeline (mv_gemm256.hip,
+// AMODE 3) — decided by K alone so that mv_conv3x3_partials(M, K) matches the launch
+static bool conv256_route(int K) {
+  static const bool on = [] {
+    const char* e = std::getenv("MIVOD_CONV256");
+    return !(e && e[0] == '0');
+  }();
+  return on && K % 256 == 0 && K <= 2048;
+}
+
 int64_t mv_conv3x3_partials(int64_t M, int K) {
   using namespace mv::conv;
+  if (conv256_route(K)) return mv_gemm256_partials(M, K);
   if (conv_bn_of(K) == 128)
     return streams_for<128, true>((M + Cfg<128, true>::BM - 1) / Cfg<128, true>::BM, K / 128);
   return streams_for<64, true>((M + Cfg<64, true>::BM - 1) / Cfg<64, true>::BM, K / 64);
@@ -420,6 +431,8 @@ bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, in
     }
     return mv_conv64(x, w, y, N, H, W, shift, partial, grid, st, bn_x, bn_vec);
   }
+  if (conv256_route(K))      // (a shape it cannot take is an error: the partial rows differ)
+    return mv_conv256(x, w, y, N, H, W, C, K, ks, stride, shift, partial, bn_x, bn_vec, st);
   Geo g;
   g.ks = ks;
   g.H = H;
@@ -626,6 +639,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 }  // namespace conv
 }  // namespace mv
 
+namespace mv {
+namespace conv {
+template <int PS, typename TO>
+__global__ void wgrad1x1_reduce_kernel(const float* __restrict__ partial, TO* __restrict__ dw,
+                                       int64_t E, int P);
+}  // namespace conv
+}  // namespace mv
+
 static int wgrad_msplit(int64_t nchunks, int nkc) {
   const char* e = std::getenv("MIVOD_WGRAD_BLOCKS");       // workgroups per launch (A/B)
   const int64_t target = e && std::atoi(e) > 0 ? std::atoi(e) : 512;
@@ -635,10 +656,25 @@ static int wgrad_msplit(int64_t nchunks, int nkc) {
   return (int)ms;
 }
 
+// C, K % 256 == 0 (ResNet-50 layers 3-4): the 256 x 256 pipeline (mv_gemm256.hip
+// wgrad256_kernel<9>: one tap's 256 x 256 (k, c) block per tile, X rows gathered)
+static bool w256_3x3_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MIVOD_WGRAD256_3X3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int64_t mv_wgrad3x3_workspace(int64_t M, int K, int C) {
   const int nkc = (K / 64) * (C / 64);
   const int64_t nchunks = (M + 31) / 32;
-  return (int64_t)wgrad_msplit(nchunks, nkc) * 9 * K * C;
+  int64_t n = (int64_t)wgrad_msplit(nchunks, nkc) * 9 * K * C;
+  if (C % 256 == 0 && K % 256 == 0) {
+    const int64_t n256 = mv_wgrad256_splits(M, 9 * C, K) * 9 * K * C;
+    n = n256 > n ? n256 : n;
+  }
+  return n;
 }
 
 bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
@@ -657,6 +693,15 @@ bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, in
   const int nkc = (K / 64) * (C / 64);
   const int64_t nchunks = (g.M + 31) / 32;
   const int ms = wgrad_msplit(nchunks, nkc);
+  if (w256_3x3_on() && mv_wgrad256_3x3_supported(N, H, W, C, K, stride) &&
+      mv_wgrad256_3x3(x, dy, work, N, H, W, C, K, stride, st)) {
+    const int P = (int)mv_wgrad256_3x3_splits(N, H, W, C, K, stride);
+    const int64_t E = (int64_t)9 * K * C;       // [K][9][C] = the channels_last filter
+    hipLaunchKernelGGL((wgrad1x1_reduce_kernel<16, __bf16>),
+                       dim3((unsigned)((E / 4 + 256 / 16 - 1) / (256 / 16))), dim3(256), 0, st,
+                       (const float*)work, (__bf16*)dw, E, P);
+    return true;
+  }
   static const bool w64 = [] {
     const char* e = std::getenv("MIVOD_WGRAD64");
     return !(e && e[0] == '0');

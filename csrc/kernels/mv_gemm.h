@@ -58,18 +58,18 @@ bool mv_gemm_nt_apply_dual(const void* A, const void* B, const void* A2, const v
                            const float* rscale, const float* rbias, void* mask, hipStream_t st);
 
 // 256 x 256 tile, 8-wave glds pipeline (mv_gemm256.hip): N % 256 == 0, K % 64 == 0;
-// partial rows = mv_gemm256_partials(M).  mv_gemm_nt routes its tiled shapes here.
+// partial rows = mv_gemm256_partials(M, N).  mv_gemm_nt routes its tiled shapes here.
 bool mv_gemm256_supported(int64_t M, int N, int K);
-int64_t mv_gemm256_partials(int64_t M);
+int64_t mv_gemm256_partials(int64_t M, int N);
 bool mv_gemm256_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
                    const float* shift, float* partial, hipStream_t st);
 // The strided 1x1 conv (stride ds) on the same kernel: X [Nb, H, W, K] NHWC, C [Nb * Ho *
-// Wo, N]; optional BN statistics (partial rows = mv_gemm256_partials(Nb * Ho * Wo)).
+// Wo, N]; optional BN statistics (partial rows = mv_gemm256_partials(Nb * Ho * Wo, N)).
 bool mv_gemm256_strided(const void* X, const void* B, void* C, int Nb, int H, int W, int K, int N,
                         int ds, const float* shift, float* partial, hipStream_t st);
 // D = [A1 | A2] . B^T + badd (A1 [M, K1], A2 [M, K2], B [N, K1 + K2]); with partial: the
 // BN fold's data-gradient epilogue (mv_gemm_fold_dx's, any N % 256 == 0): d = fma(xb,
-// scale, bias) > 0 ? bf16(D) : 0 is stored, partials [mv_gemm256_partials(M)][2][N] =
+// scale, bias) > 0 ? bf16(D) : 0 is stored, partials [mv_gemm256_partials(M, N)][2][N] =
 // (sum d, sum d (xb - mean)); without: plain store
 bool mv_gemm256_dual(const void* A1, const void* A2, const void* B, const float* badd, void* D,
                      int64_t M, int K1, int K2, int N, const void* xb, const float* mean,
@@ -80,3 +80,20 @@ bool mv_wgrad256_supported(int64_t M, int C, int K, int k1);
 int64_t mv_wgrad256_splits(int64_t M, int C, int K);
 bool mv_wgrad256(const void* X, const void* DY, const void* DY2, float* partial, int64_t M, int C,
                  int K, int k1, hipStream_t st);
+// Implicit ks x ks convolution (pad ks / 2, stride 1-2, ks = 1 or 3) on the same pipeline
+// (AMODE 3): X [Nb, H, W, Cin] NHWC, Wt [Cout][ks][ks][Cin], Y [Nb * Ho * Wo, Cout];
+// Cout % 256 == 0.  partial: BN statistics of Y around shift (rows = mv_gemm256_partials(M, Cout));
+// bn_x (+ partial, bn_vec = [4][Cout] mean, -, scale, bias): Y is the data gradient of a
+// BN+ReLU output and d = fma(bn_x, scale, bias) > 0 ? bf16(Y) : 0 is stored with the
+// partials (sum d, sum d (bn_x - mean)) — mv_conv.hip's EPI 2.
+bool mv_conv256_supported(int N, int H, int W, int Cin, int Cout, int ks, int stride);
+bool mv_conv256(const void* X, const void* Wt, void* Y, int Nb, int H, int W, int Cin, int Cout,
+                int ks, int stride, const float* shift, float* partial, const void* bn_x,
+                const float* bn_vec, hipStream_t st);
+// 3x3 (pad 1, stride 1-2) weight gradient on the same pipeline: partial[S][K][9 C] fp32
+// ([K][3][3][C] per split, the channels_last filter layout), S = mv_wgrad256_3x3_splits;
+// C % 256 == 0, K % 256 == 0
+bool mv_wgrad256_3x3_supported(int N, int H, int W, int C, int K, int stride);
+int64_t mv_wgrad256_3x3_splits(int N, int H, int W, int C, int K, int stride);
+bool mv_wgrad256_3x3(const void* X, const void* DY, float* partial, int N, int H, int W, int C,
+                     int K, int stride, hipStream_t st);

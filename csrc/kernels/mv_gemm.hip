@@ -763,14 +763,14 @@ static bool g256_first(int64_t M, int N, int K) {
 // number of [2][N] statistics partial rows gemm_nt writes for this problem
 int64_t mv_gemm_partials(int64_t M, int N, int K) {
   int bn;
-  if (g256_first(M, N, K)) return mv_gemm256_partials(M);
+  if (g256_first(M, N, K)) return mv_gemm256_partials(M, N);
   if (stream_cfg(K, N, &bn)) {
 #define MV_P(KK, BB) \
     if (K == KK && bn == BB) return streams_for<KK, BB, 1>(M, N);
     MV_STREAM_CASES(MV_P)
 #undef MV_P
   }
-  if (gemm256_on() && mv_gemm256_supported(M, N, K)) return mv_gemm256_partials(M);
+  if (gemm256_on() && mv_gemm256_supported(M, N, K)) return mv_gemm256_partials(M, N);
   const int bm = N % 128 == 0 ? 128 : 256;
   return (M + bm - 1) / bm;
 }
@@ -891,7 +891,7 @@ int64_t mv_gemm_fold_dx_partials(int64_t M, int K1, int K2) {
   int64_t P = -1;
   mv::gemm::BwdEpi e{};
   if (!fold_dx_dispatch(K1, K2, nullptr, nullptr, nullptr, M, K2, e, nullptr, &P, nullptr))
-    return fold_dx_g256(M, K1, K2) ? mv_gemm256_partials(M) : -1;
+    return fold_dx_g256(M, K1, K2) ? mv_gemm256_partials(M, K2) : -1;
   return P;
 }
 

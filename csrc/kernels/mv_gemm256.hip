@@ -76,10 +76,16 @@ __device__ __forceinline__ void barrier() {
 
 // Kernel arguments.  A modes: 0 plain A[M, K]; 1 strided gather (a stride-ds 1x1 conv:
 // A is the [*, H, W, K] input, output row (n, ho, wo) reads input row (n, ho ds, wo ds));
-// 2 dual source (A columns [0, K1) from A [M, K1], [K1, K) from A2 [M, K - K1]).
+// 2 dual source (A columns [0, K1) from A [M, K1], [K1, K) from A2 [M, K - K1]);
+// 3 implicit ks x ks convolution (pad ks / 2, stride ds, ks = 1 or 3): A = im2col of the
+// [*, H, W, Cin] input, never materialised — K tile kt is channels [c0, c0 + 64) of filter
+// tap kt / (Cin / 64); each staged row carries its tap-(0, 0) address and a 9-bit mask of
+// the taps inside the image (padding taps read a zero page); B = the [N][ks][ks][Cin]
+// filter, already K-contiguous.
 // Epilogues: 0 plain; 1 + BN statistics of the bf16 C around shift; 4 the BN fold's data
-// gradient (mv_gemm.hip EPI 4): C + badd, d = fma(xb, sc, bi) > 0 ? bf16 : 0 is stored,
-// partials (sum d, sum d (xb - mean)); 6 C + badd, plain store.
+// gradient (mv_gemm.hip EPI 4): C + badd (badd may be null: the 3x3 data gradient with the
+// producing BN+ReLU's backward reduce, mv_conv.hip EPI 2), d = fma(xb, sc, bi) > 0 ? bf16 : 0
+// is stored, partials (sum d, sum d (xb - mean)); 6 C + badd, plain store.
 struct Args {
   const __bf16* A;
   const __bf16* A2;
@@ -89,6 +95,7 @@ struct Args {
   int N, K, K1, ntn;
   int64_t ntiles;
   int ds, H, W, Ho, Wo;
+  int Cin, ks;                    // AMODE 3
   const float* shift;
   float* partial;
   const float* badd;
@@ -102,8 +109,18 @@ template <int EPI>
 constexpr int nvec() { return EPI == 1 ? 1 : EPI == 4 ? 4 : EPI == 6 ? 1 : 0; }
 constexpr int kVecFloats = 8192;          // LDS for the per-channel epilogue vectors (32 KB)
 
-template <int EPI, int AMODE>
+// zero page: padding taps (AMODE 3) and rows past M (the weight gradient)
+__device__ __attribute__((aligned(16))) uint32_t g_w256_zero[64];
+
+// MT: m tiles (16 rows) per wave group — 8 (BM = 256) or 7 (BM = 224: ResNet-50's
+// M = 2048 x 196 / x 49 split into 1792 / 448 row blocks, a whole number of rounds over 256
+// CUs for every N tile count, where 256-row blocks leave a 1/8- to 1/2-full last round).
+// With MT = 7 the second A half-tile holds 48 live rows (the other 16 re-stage live rows,
+// never read).
+template <int EPI, int AMODE, int MT>
 __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
+  constexpr int BMv = MT * 32;
+  constexpr int MH1 = MT - 4;               // m tiles in A half 1
   constexpr int NV = nvec<EPI>();
   constexpr bool STATS = EPI == 1 || EPI == 4;
   constexpr bool BADD = EPI == 4 || EPI == 6;
@@ -127,8 +144,13 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   // columns {64 q + 32 h + j}.  Byte offsets at K offset 0 (the host checks < 4 GB).
   // (dual source: the A row index instead, both sources' offsets formed at issue)
   uint32_t offa[2][2], offb[2][2];
+  uint32_t abase[2][2];            // AMODE 3: tap-(0, 0) byte offset of the row's chunk in
+                                   // A (mod 2^32: negative at the top-left padding, only
+                                   // used with a tap that lands inside the image)
+  uint32_t avalid[2];              // AMODE 3: taps inside the image, row i at bit 16 i
   const uint32_t scb = (uint32_t)(((lane & 7) ^ ((lane >> 3) & 7)) * 16);   // = sc * 16 bytes
   const int KT = p.K / BK, KT1 = AMODE == 2 ? p.K1 / BK : KT;
+  const int csteps = AMODE == 3 ? p.Cin / BK : 1;
   auto set_src = [&](int64_t tl) {
     const int64_t mt = tl / p.ntn;
     const int nt = (int)(tl - mt * p.ntn);
@@ -138,7 +160,9 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
       const int sc = (lane & 7) ^ (r & 7);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        int64_t row = mt * BM + (r >> 6) * 128 + h * 64 + (r & 63);
+        const int rr = (r & 63);
+        int64_t row = mt * BMv + (r >> 6) * (MT * 16) + h * 64 +
+                      ((h == 1 && rr >= 16 * MH1) ? rr - 16 * MH1 : rr);
         row = row < p.M ? row : p.M - 1;           // rows past M: a valid row, never stored
         if constexpr (AMODE == 1) {
           const int64_t hw = (int64_t)p.Ho * p.Wo;
@@ -146,6 +170,27 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
           const int rem = (int)(row - n * hw);
           const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
           row = (n * p.H + (int64_t)ho * p.ds) * p.W + (int64_t)wo * p.ds;
+        }
+        if constexpr (AMODE == 3) {
+          const int64_t hw = (int64_t)p.Ho * p.Wo;
+          const int64_t n = row / hw;
+          const int rem = (int)(row - n * hw);
+          const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+          const int pad = p.ks >> 1;
+          const int hi0 = ho * p.ds - pad, wi0 = wo * p.ds - pad;
+          uint32_t v = 0;
+#pragma unroll
+          for (int tr = 0; tr < 3; ++tr)
+#pragma unroll
+            for (int ts = 0; ts < 3; ++ts) {
+              const bool ok = tr < p.ks && ts < p.ks && (unsigned)(hi0 + tr) < (unsigned)p.H &&
+                              (unsigned)(wi0 + ts) < (unsigned)p.W;
+              v |= (ok ? 1u : 0u) << (tr * p.ks + ts);
+            }
+          if (i == 0) avalid[h] = v;
+          else avalid[h] |= v << 16;
+          abase[h][i] =
+              (uint32_t)(((((int64_t)n * p.H + hi0) * p.W + wi0) * p.Cin + sc * 8) * 2);
         }
         if constexpr (AMODE == 2) {
           offa[h][i] = (uint32_t)row;
@@ -158,11 +203,25 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
     }
   };
   auto issue = [&](int slot, int buf, int kt) {
+    // AMODE 3: the K tile's filter tap and channel block (wave-uniform)
+    uint32_t toff = 0;
+    int tap = 0;
+    if constexpr (AMODE == 3) {
+      tap = kt / csteps;
+      const int c0 = (kt - tap * csteps) * BK;
+      const int tr = tap / p.ks, ts = tap - tr * p.ks;
+      toff = (uint32_t)(((tr * p.W + ts) * p.Cin + c0) * 2);
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const char* src;
       if (slot >= 2) {
         src = reinterpret_cast<const char*>(p.B) + offb[slot - 2][i] + kt * (BK * 2);
+      } else if (AMODE == 3) {
+        // (padding taps: every lane reads the same zero chunk — the DMA writes lane * 16)
+        src = ((avalid[slot] >> (tap + 16 * i)) & 1u)
+                  ? reinterpret_cast<const char*>(p.A) + (uint32_t)(abase[slot][i] + toff)
+                  : reinterpret_cast<const char*>(g_w256_zero);
       } else if (AMODE == 2) {
         src = kt < KT1 ? reinterpret_cast<const char*>(p.A) + offa[slot][i] * (uint32_t)(p.K1 * 2) +
                              scb + kt * (BK * 2)
@@ -188,9 +247,10 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
     const __bf16* base = smem + buf * BUF + h * HALF;
 #pragma unroll
     for (int b = 0; b < 4; ++b)
+      if (h == 0 || b < MH1)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        af[b][kk] = *reinterpret_cast<const bf16x8*>(base + swz(wm * 64 + b * 16 + rl, kk * 4 + g));
+        for (int kk = 0; kk < 2; ++kk)
+          af[b][kk] = *reinterpret_cast<const bf16x8*>(base + swz(wm * 64 + b * 16 + rl, kk * 4 + g));
   };
   auto read_b = [&](int buf, int h) {
     const __bf16* base = smem + buf * BUF + (2 + h) * HALF;
@@ -208,7 +268,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b)
-          acc[qn * 2 + a][qm * 4 + b] = mfma(bfr[qn][a][kk], af[b][kk], acc[qn * 2 + a][qm * 4 + b]);
+          if (qm == 0 || b < MH1)
+            acc[qn * 2 + a][qm * 4 + b] = mfma(bfr[qn][a][kk], af[b][kk], acc[qn * 2 + a][qm * 4 + b]);
     __builtin_amdgcn_s_setprio(0);
   };
   // C rows of this tile (+ the epilogue's statistics partial row (mt, wm)); no barrier:
@@ -222,7 +283,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   auto epilogue = [&](int64_t tl) {
     const int64_t mt = tl / p.ntn;
     const int n0 = (int)(tl - mt * p.ntn) * BN;
-    const int64_t m0 = mt * BM;
+    const int64_t m0 = mt * BMv;
     float s1[2][8], s2[2][8];
 #pragma unroll
     for (int q = 0; q < 2; ++q)
@@ -231,9 +292,26 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
         s1[q][j] = 0.f;
         s2[q][j] = 0.f;
       }
+    // EPI 4: every BN-input row of the tile is loaded before the first store (the stores
+    // may alias xb for the compiler: loads issued inside the loop each wait out a full
+    // memory latency behind the previous store — ~100 us per 3x3 data gradient)
+    // (in batches of 2 row blocks: 16 VGPRs — 4 blocks already spill at 256 VGPRs)
+    uint4 xr[2][2];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const int64_t row = m0 + wm * 128 + b * 16 + rl;
+    for (int b = 0; b < MT; ++b) {
+      if (EPI == 4 && (b & 1) == 0) {
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          const int64_t row = m0 + wm * (MT * 16) + (b + bb) * 16 + rl;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int c0 = n0 + wn * 64 + q * 32 + (g & 1) * 16 + (g >> 1) * 8;
+            xr[bb][q] = (b + bb < MT && row < p.M) ? *reinterpret_cast<const uint4*>(p.xb + row * N + c0)
+                                  : uint4{0u, 0u, 0u, 0u};
+          }
+        }
+      }
+      const int64_t row = m0 + wm * (MT * 16) + b * 16 + rl;
       const bool in = row < p.M;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -265,8 +343,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
         }
         if constexpr (EPI == 4) {
           if (in) {
-            const uint4 xr = *reinterpret_cast<const uint4*>(p.xb + row * N + c0);
-            const uint32_t xw[4] = {xr.x, xr.y, xr.z, xr.w};
+            const uint32_t xw[4] = {xr[b & 1][q].x, xr[b & 1][q].y, xr[b & 1][q].z, xr[b & 1][q].w};
             const float* mean = vecs + N;
             const float* scv = vecs + 2 * N;
             const float* biv = vecs + 3 * N;
@@ -325,7 +402,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   if constexpr (NV > 0) {
     for (int c = tid; c < N; c += NT) {
       if constexpr (EPI == 1) vecs[c] = p.shift ? p.shift[c] : 0.f;
-      if constexpr (BADD) vecs[c] = p.badd[c];
+      if constexpr (BADD) vecs[c] = p.badd ? p.badd[c] : 0.f;
       if constexpr (EPI == 4) {
         vecs[N + c] = p.mean[c];
         vecs[2 * N + c] = p.sc[c];
@@ -438,7 +515,6 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
 // c of one k — 16-byte partial stores.  Waves 2 (c) x 4 (k), 128 c x 64 k per wave, the
 // 4-phase / one-barrier-stagger K loop of gemm256_kernel.
 // ===========================================================================
-__device__ __attribute__((aligned(16))) uint32_t g_w256_zero[64];     // zero page (rows >= M)
 
 struct WArgs {
   const __bf16* X;
@@ -448,6 +524,10 @@ struct WArgs {
   int64_t M;
   int C, K, k1, ntc, ntiles, ms;
   int64_t per;                  // 64-pixel chunks per split
+  // TAPS = 9 (3x3, pad 1, stride ds): the output columns are (tap, c) — C = 9 Cx, a 256-
+  // column tile is 256 channels of ONE tap (Cx % 256 == 0) — and X rows are gathered:
+  // output pixel (n, ho, wo) reads input pixel (n, ho ds - 1 + r, wo ds - 1 + s)
+  int Cx, H, W, Ho, Wo, ds;
 };
 
 __device__ __forceinline__ int wf(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
@@ -471,6 +551,7 @@ __device__ __forceinline__ bf16x8 trp(const __bf16* pa, const __bf16* pb) {
   return __builtin_bit_cast(bf16x8, o);
 }
 
+template <int TAPS>
 __global__ __launch_bounds__(NT, 1) void wgrad256_kernel(WArgs p) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -480,6 +561,10 @@ __global__ __launch_bounds__(NT, 1) void wgrad256_kernel(WArgs p) {
   const int t = remap(blockIdx.x, gridDim.x);
   const int split = t / p.ntiles, tl = t - split * p.ntiles;
   const int c0 = (tl % p.ntc) * 256, k0 = (tl / p.ntc) * 256;
+  // TAPS = 9: this tile's filter tap and its channel block in X
+  const int tap = TAPS == 9 ? c0 / p.Cx : 0;
+  const int xc0 = TAPS == 9 ? c0 - tap * p.Cx : c0;
+  const int tr = tap / 3, ts = tap - 3 * (tap / 3);
   const int64_t mb = (int64_t)split * p.per * BK;
   int64_t me = mb + p.per * BK;
   me = me < p.M ? me : p.M;
@@ -499,19 +584,40 @@ __global__ __launch_bounds__(NT, 1) void wgrad256_kernel(WArgs p) {
     const int lc = (lane & 15) ^ wf(r);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      choff[h][i] = c0 + 128 * (lc >> 3) + 64 * h + 8 * (lc & 7);          // X half h
+      choff[h][i] = xc0 + 128 * (lc >> 3) + 64 * h + 8 * (lc & 7);         // X half h
       choff[2 + h][i] = kb + 64 * (lc >> 2) + 32 * h + 8 * (lc & 3);       // DY half h
     }
   }
   srcb[0] = srcb[1] = p.X;
   srcb[2] = srcb[3] = dyb;
+  // TAPS = 9: the gathered X pixel of each staged row (-1: padding or past M), formed at
+  // the K tile's first X half (slot 0) and reused by the second (slot 1)
+  int64_t xpix[2] = {-1, -1};
   auto issue = [&](int slot, int buf, int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int64_t row = mb + (int64_t)kt * BK + (2 * w + i) * 4 + (lane >> 4);
-      const int ld = slot < 2 ? p.C : ldy;
-      const void* src = row < me ? (const void*)(srcb[slot] + row * ld + choff[slot][i])
-                                 : (const void*)(g_w256_zero + (lane & 15) * 4);
+      const void* src;
+      if (TAPS == 9 && slot < 2) {
+        if (slot == 0) {
+          xpix[i] = -1;
+          if (row < me) {            // (M < 2^31: 32-bit unsigned divisions)
+            const uint32_t r32 = (uint32_t)row, hw = (uint32_t)(p.Ho * p.Wo);
+            const uint32_t n = r32 / hw;
+            const uint32_t rem = r32 - n * hw;
+            const uint32_t ho = rem / (uint32_t)p.Wo, wo = rem - ho * (uint32_t)p.Wo;
+            const int hi = (int)ho * p.ds - 1 + tr, wi = (int)wo * p.ds - 1 + ts;
+            if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+              xpix[i] = ((int64_t)n * p.H + hi) * p.W + wi;
+          }
+        }
+        src = xpix[i] >= 0 ? (const void*)(p.X + xpix[i] * p.Cx + choff[slot][i])
+                           : (const void*)(g_w256_zero + (lane & 15) * 4);
+      } else {
+        const int ld = slot < 2 ? p.C : ldy;
+        src = row < me ? (const void*)(srcb[slot] + row * ld + choff[slot][i])
+                       : (const void*)(g_w256_zero + (lane & 15) * 4);
+      }
       glds16(src, smem + buf * BUF + slot * HALF + (2 * w + i) * 512);
     }
   };
@@ -631,23 +737,42 @@ static int g256_cus() {
   return n;
 }
 
+// 224-row blocks when they tile M exactly and there is one column tile (N = 256: ResNet-50
+// layer 3's 1024 -> 256 1x1 convs, 251 -> 238 us; with 2+ column tiles 256 rows measured
+// faster, and the 3x3 convs' long K leaves them level) — see gemm256_kernel's MT;
+// MIVOD_G256_BM=256 forces 256
+static int g256_bm(int64_t M, int N) {
+  static const bool allow224 = [] {
+    const char* e = std::getenv("MIVOD_G256_BM");
+    return !(e && std::atoi(e) == 256);
+  }();
+  return allow224 && N == 256 && M % 224 == 0 ? 224 : 256;
+}
+
 bool mv_gemm256_supported(int64_t M, int N, int K) {
   return M > 0 && N % 256 == 0 && K % 64 == 0 && K >= 64 &&
          (M + 255) / 256 * (N / 256) < (int64_t(1) << 31) && M * K * 2 < (int64_t(1) << 32) &&
          (int64_t)N * K * 2 < (int64_t(1) << 32);
 }
 
-// two statistics rows (one per M wave group) per 256-row block
-int64_t mv_gemm256_partials(int64_t M) { return 2 * ((M + 255) / 256); }
+// two statistics rows (one per M wave group) per row block
+int64_t mv_gemm256_partials(int64_t M, int N) {
+  const int bm = g256_bm(M, N);
+  return 2 * ((M + bm - 1) / bm);
+}
 
 template <int EPI, int AMODE>
 static void g256_launch(mv::g256::Args a, hipStream_t st) {
   using namespace mv::g256;
+  const int bm = g256_bm(a.M, a.N);
   a.ntn = a.N / BN;
-  a.ntiles = (a.M + BM - 1) / BM * a.ntn;
+  a.ntiles = (a.M + bm - 1) / bm * a.ntn;
   const int cus = g256_cus();
   const dim3 grid((unsigned)(a.ntiles < cus ? a.ntiles : cus));
-  hipLaunchKernelGGL((gemm256_kernel<EPI, AMODE>), grid, dim3(NT), 0, st, a);
+  if (bm == 224)
+    hipLaunchKernelGGL((gemm256_kernel<EPI, AMODE, 7>), grid, dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<EPI, AMODE, 8>), grid, dim3(NT), 0, st, a);
 }
 
 bool mv_gemm256_nt(const void* A, const void* B, void* C, int64_t M, int N, int K,
@@ -722,6 +847,53 @@ bool mv_gemm256_dual(const void* A1, const void* A2, const void* B, const float*
   return true;
 }
 
+// ---------------------------------------------------------------- implicit ks x ks conv
+bool mv_conv256_supported(int N, int H, int W, int Cin, int Cout, int ks, int stride) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const int64_t M = (int64_t)N * Ho * Wo;
+  // (A rows are 32-bit byte offsets: the input must stay below 4 GB)
+  return (ks == 1 || ks == 3) && stride >= 1 && stride <= 2 && Cin % 64 == 0 && Cin > 0 &&
+         (int64_t)N * H * W * Cin * 2 < (int64_t(1) << 32) &&
+         Cout % 256 == 0 && Cout <= mv::g256::kVecFloats / 4 && M > 0 &&
+         (M + 255) / 256 * (Cout / 256) < (int64_t(1) << 31) &&
+         (int64_t)Cout * ks * ks * Cin * 2 < (int64_t(1) << 32);
+}
+
+bool mv_conv256(const void* X, const void* Wt, void* Y, int Nb, int H, int W, int Cin, int Cout,
+                int ks, int stride, const float* shift, float* partial, const void* bn_x,
+                const float* bn_vec, hipStream_t st) {
+  using namespace mv::g256;
+  if (!mv_conv256_supported(Nb, H, W, Cin, Cout, ks, stride) || (bn_x && !partial)) return false;
+  Args a{};
+  a.A = (const __bf16*)X;
+  a.B = (const __bf16*)Wt;
+  a.C = (__bf16*)Y;
+  a.Ho = (H - 1) / stride + 1;
+  a.Wo = (W - 1) / stride + 1;
+  a.M = (int64_t)Nb * a.Ho * a.Wo;
+  a.N = Cout;
+  a.K = ks * ks * Cin;
+  a.ds = stride;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.ks = ks;
+  a.shift = shift;
+  a.partial = partial;
+  if (bn_x) {         // data gradient + the producing BN+ReLU's backward reduce ([4][Cout] vec)
+    a.xb = (const __bf16*)bn_x;
+    a.mean = bn_vec;
+    a.sc = bn_vec + 2 * Cout;
+    a.bi = bn_vec + 3 * Cout;
+    g256_launch<4, 3>(a, st);
+  } else if (partial) {
+    g256_launch<1, 3>(a, st);
+  } else {
+    g256_launch<0, 3>(a, st);
+  }
+  return true;
+}
+
 // ---------------------------------------------------------------- 1x1 weight gradient
 bool mv_wgrad256_supported(int64_t M, int C, int K, int k1) {
   return M > 0 && C % 256 == 0 && K % 256 == 0 && k1 > 0 && k1 <= K && k1 % 256 == 0 &&
@@ -761,6 +933,43 @@ bool mv_wgrad256(const void* X, const void* DY, const void* DY2, float* partial,
   a.ntc = C / 256;
   a.ntiles = (C / 256) * (K / 256);
   w256_split(M, C, K, &a.ms, &a.per);
-  hipLaunchKernelGGL(wgrad256_kernel, dim3((unsigned)(a.ntiles * a.ms)), dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(wgrad256_kernel<1>, dim3((unsigned)(a.ntiles * a.ms)), dim3(NT), 0, st, a);
+  return true;
+}
+
+// ---------------------------------------------------------------- 3x3 weight gradient
+bool mv_wgrad256_3x3_supported(int N, int H, int W, int C, int K, int stride) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  return N > 0 && (stride == 1 || stride == 2) && C % 256 == 0 && K % 256 == 0 &&
+         mv_wgrad256_supported((int64_t)N * Ho * Wo, 9 * C, K, K);
+}
+
+int64_t mv_wgrad256_3x3_splits(int N, int H, int W, int C, int K, int stride) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  return mv_wgrad256_splits((int64_t)N * Ho * Wo, 9 * C, K);
+}
+
+bool mv_wgrad256_3x3(const void* X, const void* DY, float* partial, int N, int H, int W, int C,
+                     int K, int stride, hipStream_t st) {
+  using namespace mv::g256;
+  if (!mv_wgrad256_3x3_supported(N, H, W, C, K, stride)) return false;
+  WArgs a{};
+  a.X = (const __bf16*)X;
+  a.DY = (const __bf16*)DY;
+  a.partial = partial;
+  a.Ho = (H - 1) / stride + 1;
+  a.Wo = (W - 1) / stride + 1;
+  a.M = (int64_t)N * a.Ho * a.Wo;
+  a.C = 9 * C;
+  a.K = K;
+  a.k1 = K;
+  a.Cx = C;
+  a.H = H;
+  a.W = W;
+  a.ds = stride;
+  a.ntc = a.C / 256;
+  a.ntiles = (a.C / 256) * (K / 256);
+  w256_split(a.M, a.C, K, &a.ms, &a.per);
+  hipLaunchKernelGGL(wgrad256_kernel<9>, dim3((unsigned)(a.ntiles * a.ms)), dim3(NT), 0, st, a);
   return true;
 }

@@ -266,6 +266,10 @@ def _dgrad_on_mivod(cin: int, cout: int) -> bool:
         return False
     if v == "1":
         return True
+    # the data gradient's output channels (cin) % 256 == 0: the 256 x 256 pipeline
+    # (mv_gemm256.hip AMODE 3) — ahead of CK's forward solver on layers 3-4
+    if cin % 256 == 0 and cin <= 2048 and os.environ.get("MIVOD_CONV256", "1") != "0":
+        return True
     return max(cin, cout) <= int(v)
 
 
@@ -273,8 +277,12 @@ def _wgrad_on_mivod(cin: int, cout: int, stride: int) -> bool:
     """mivod's 3x3 weight-gradient kernel (csrc/kernels/mv_conv.hip wgrad3x3_kernel) beats
     MIOpen's on every ResNet-50 conv2 shape except the 512-channel stride-2 one
     (scripts/micro_conv3x3.py: 608-793 vs 393-743 TF/s)."""
-    return (os.environ.get("MIVOD_WGRAD3X3", "1") != "0"
-            and not (stride == 2 and max(cin, cout) >= 512))
+    if os.environ.get("MIVOD_WGRAD3X3", "1") == "0":
+        return False
+    # C, K % 256 == 0: the 256 x 256 pipeline (mv_gemm256.hip wgrad256_kernel<9>), any stride
+    if cin % 256 == 0 and cout % 256 == 0 and os.environ.get("MIVOD_WGRAD256_3X3", "1") != "0":
+        return True
+    return not (stride == 2 and max(cin, cout) >= 512)
 
 
 class _Conv3x3(torch.autograd.Function):

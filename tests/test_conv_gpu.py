@@ -25,7 +25,16 @@ def _cl(t):
                                          # row (62), 1-pixel rows, and W = 63 (falls back)
                                          (3, 64, 13, 9, 64, 1), (1, 64, 17, 62, 64, 1),
                                          (2, 64, 5, 1, 64, 1), (1, 64, 8, 63, 64, 1),
-                                         (9, 64, 56, 56, 64, 1)])
+                                         (9, 64, 56, 56, 64, 1),
+                                         # Cout % 256 == 0 = the 256 x 256 pipeline
+                                         # (mv_gemm256.hip AMODE 3): stride 2, odd sizes,
+                                         # small Cin, several N tiles, partial last M tile
+                                         (3, 256, 14, 14, 256, 2), (2, 64, 9, 11, 256, 1),
+                                         (5, 512, 7, 7, 512, 2), (9, 256, 14, 14, 512, 1),
+                                         (3, 128, 13, 5, 768, 2),
+                                         # N * Ho * Wo % 224 == 0: 224-row blocks
+                                         (8, 256, 14, 14, 256, 1), (8, 256, 28, 28, 512, 2),
+                                         (32, 512, 7, 7, 512, 1)])
 def test_conv3x3_matches_fp32(cuda, n, c, h, w, k, s):
     nat = _nat()
     g = torch.Generator(device=cuda).manual_seed(n * 1000 + c + h + k + s)
@@ -112,13 +121,15 @@ def test_resnet_bottleneck_uses_conv3x3(cuda):
 
 
 @pytest.mark.parametrize("c,k,ks", [(64, 64, 3), (128, 128, 3), (64, 128, 3), (64, 256, 1),
-                                    (128, 512, 1), (512, 2048, 1)])
-def test_conv3x3_bn_bwd_matches_reference(cuda, c, k, ks):
+                                    (128, 512, 1), (512, 2048, 1),
+                                    # output channels % 256 == 0: mv_gemm256.hip AMODE 3 + EPI 4
+                                    (256, 256, 3), (512, 512, 3), (256, 64, 3), (512, 128, 1)])
+@pytest.mark.parametrize("n,h,w", [(3, 11, 9), (32, 7, 7)])    # M = 1568: 224-row blocks
+def test_conv3x3_bn_bwd_matches_reference(cuda, c, k, ks, n, h, w):
     """dgrad (forward conv with the transposed filter; 3x3 or 1x1) + mode-1 BN backward
     reduce in the epilogue == conv2d + relu mask + (sum d, sum d (x - mean)) in fp32."""
     nat = _nat()
-    g = torch.Generator(device=cuda).manual_seed(c + 7 * k)
-    n, h, w = 3, 11, 9
+    g = torch.Generator(device=cuda).manual_seed(c + 7 * k + n)
     dy = _cl(torch.randn(n, k, h, w, device=cuda, generator=g).to(torch.bfloat16))
     wt = _cl((torch.randn(c, k, ks, ks, device=cuda, generator=g) / (ks * ks * k) ** 0.5).to(
         torch.bfloat16))
@@ -161,7 +172,11 @@ def test_resnet_uses_conv3x3_bwd_fusion(cuda, monkeypatch):
                                          (2, 64, 128, 8, 8, 1), (1, 256, 64, 7, 7, 1),
                                          (2, 64, 64, 9, 8, 1), (1, 64, 64, 3, 4, 1),
                                          (3, 64, 64, 13, 28, 1), (2, 64, 64, 56, 56, 1),
-                                         (5, 64, 64, 17, 52, 1)])
+                                         (5, 64, 64, 17, 52, 1),
+                                         # C, K % 256 == 0: mv_gemm256.hip wgrad256_kernel<9>
+                                         (2, 256, 256, 9, 7, 1), (3, 256, 512, 10, 10, 2),
+                                         (2, 512, 256, 7, 7, 1), (9, 256, 256, 14, 14, 1),
+                                         (4, 512, 512, 13, 13, 2)])
 def test_wgrad3x3_matches_fp32(cuda, n, c, k, h, w, s):
     nat = _nat()
     g = torch.Generator(device=cuda).manual_seed(n + c + k + h + s)

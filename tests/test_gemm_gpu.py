@@ -43,7 +43,10 @@ def test_gemm_nt_matches_fp32(cuda, M, K, N):
 
 
 @pytest.mark.parametrize("M,K,N", [(256 * 700 + 37, 64, 256), (153637, 512, 512),
-                                   (300000, 256, 1024), (4096, 2048, 2048), (255, 128, 256)])
+                                   (300000, 256, 1024), (4096, 2048, 2048), (255, 128, 256),
+                                   # M % 224 == 0: 224-row blocks (MT = 7)
+                                   (224 * 300, 1024, 256), (224 * 5, 256, 1024),
+                                   (224 * 1000, 512, 512)])
 def test_gemm256_persistent_matches_fp32(cuda, M, K, N):
     """mv_gemm256.hip: several output tiles per persistent workgroup (the next tile's
     first K tile staged during the previous epilogue), a ragged last row block, a single
