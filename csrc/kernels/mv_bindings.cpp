@@ -1471,6 +1471,55 @@ std::vector<at::Tensor> conv3x3_bn_bwd(at::Tensor dy, at::Tensor wt, at::Tensor 
   return {d, part};
 }
 
+// data gradient of a stride-2 3x3 conv (pad 1) on mv_gemm256's parity-class gather GEMM:
+// dy [N, K, H/2, W/2], wt the transposed flipped filter [C, K, 3, 3] -> dx [N, C, H, W]; with
+// (x_bn, vec): d = relu'(bn(x_bn)) * dx and the producing BN's reduce partials [P, 2, C].
+// Returns [] when the shape is not covered (the caller falls back).
+std::vector<at::Tensor> conv3x3_s2_dgrad(at::Tensor dy, at::Tensor wt, int64_t H, int64_t W,
+                                         c10::optional<at::Tensor> x_bn,
+                                         c10::optional<at::Tensor> vec) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_s2_dgrad: dy must be a channels_last bf16 GPU tensor");
+  TORCH_CHECK(wt.is_cuda() && wt.scalar_type() == at::kBFloat16 && wt.dim() == 4 &&
+                  wt.size(2) == 3 && wt.size(3) == 3 && wt.size(1) == dy.size(1) &&
+                  wt.is_contiguous(at::MemoryFormat::ChannelsLast) && wt.device() == dy.device(),
+              "conv3x3_s2_dgrad: wt must be the channels_last [C, K, 3, 3] transposed filter");
+  const int64_t N = dy.size(0), K = dy.size(1), C = wt.size(0);
+  TORCH_CHECK(H > 0 && W > 0 && (H - 1) / 2 + 1 == dy.size(2) && (W - 1) / 2 + 1 == dy.size(3),
+              "conv3x3_s2_dgrad: H, W do not match dy");
+  const bool bn = x_bn.has_value() && x_bn->defined();
+  // the BN-reduce epilogue only on the 256 x 256 pipeline (dx channels % 256 == 0)
+  if (H >= 65536 || W >= 65536 || N >= (int64_t(1) << 31) ||
+      !(bn ? mv_dgrad256_s2_supported((int)N, (int)H, (int)W, (int)C, (int)K)
+           : mv_conv3x3_s2_dgrad_supported((int)N, (int)H, (int)W, (int)C, (int)K)))
+    return {};
+  if (bn) {
+    TORCH_CHECK(x_bn->is_cuda() && x_bn->scalar_type() == at::kBFloat16 &&
+                    x_bn->sizes() == at::IntArrayRef({N, C, H, W}) &&
+                    x_bn->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    x_bn->device() == dy.device(),
+                "conv3x3_s2_dgrad: x_bn must be the BN input [N, C, H, W], channels_last bf16");
+    TORCH_CHECK(vec.has_value() && vec->is_cuda() && vec->scalar_type() == at::kFloat &&
+                    vec->is_contiguous() && vec->numel() == 4 * C && vec->device() == dy.device(),
+                "conv3x3_s2_dgrad: saved stats must be fp32 [4, C]");
+  }
+  c10::DeviceGuard guard(dy.device());
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  at::Tensor part;
+  if (bn)
+    part = at::empty({mv_dgrad256_s2_partials((int)N, (int)H, (int)W, (int)C), 2, C},
+                     dy.options().dtype(at::kFloat));
+  const bool ok = bn ? mv_dgrad256_s2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)N, (int)H,
+                                      (int)W, (int)C, (int)K, part.data_ptr<float>(),
+                                      x_bn->data_ptr(), vec->data_ptr<float>(), cur_stream())
+                     : mv_conv3x3_s2_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)N,
+                                           (int)H, (int)W, (int)C, (int)K, cur_stream());
+  TORCH_CHECK(ok, "conv3x3_s2_dgrad: launch refused");
+  if (bn) return {dx, part};
+  return {dx};
+}
+
 // weight gradient of y = conv3x3(x, w, stride, pad 1): dw [K, C, 3, 3] channels_last bf16
 at::Tensor wgrad3x3(at::Tensor x, at::Tensor dy, int64_t stride) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
@@ -1637,6 +1686,11 @@ PYBIND11_MODULE(_mvk, m) {
         py::arg("partial") = py::none());
   m.def("conv3x3_bn_bwd", &conv3x3_bn_bwd,
         "stride-1 3x3 data gradient with the producing BN+ReLU's backward reduce fused");
+  m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad,
+        "stride-2 3x3 data gradient (parity-class gather GEMMs), optionally with the producing "
+        "BN+ReLU's backward reduce; [] when the shape is not covered",
+        py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"), py::arg("x_bn") = py::none(),
+        py::arg("vec") = py::none());
   m.def("wgrad1x1", &wgrad1x1, "1x1 (pad 0, stride 1/2) conv weight gradient on MFMA",
         py::arg("x"), py::arg("dy"), py::arg("stride") = 1, py::arg("fp32_out") = false,
         py::arg("dy2") = py::none());

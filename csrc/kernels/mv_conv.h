@@ -50,3 +50,11 @@ bool mv_conv64(const void* x, const void* w, void* y, int N, int H, int W, const
 bool mv_wgrad64_supported(int N, int H, int W, int C, int K, int stride);
 bool mv_wgrad64(const void* x, const void* dy, float* partial, int grid, int N, int H, int W,
                 hipStream_t st);
+
+// Stride-2 3x3 (pad 1) data gradient as four output-parity-class gather GEMMs (no zero
+// fill, no structurally-zero products): dy [Nb, H/2, W/2, K], wt = the transposed flipped
+// filter [C][3][3][K], dx [Nb, H, W, C]; H, W even, C, K % 64 == 0 (C % 256 == 0 runs on
+// mv_gemm256.hip AMODE 4, else conv3x3_kernel's DG mode)
+bool mv_conv3x3_s2_dgrad_supported(int Nb, int H, int W, int C, int K);
+bool mv_conv3x3_s2_dgrad(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C,
+                         int K, hipStream_t st);

@@ -61,6 +61,10 @@ struct Geo {
   int H, W, C, Ho, Wo, K, st;
   int64_t M;
   int ks = 3;        // filter size: 3 (pad 1) or 1 (pad 0) for the forward kernel
+  // conv3x3_kernel<..., DG = true>: stride-2 3x3 DATA gradient, output parity class (ph, pw)
+  // (mv_gemm256.hip AMODE 4's scheme): rows are the class pixels (n, i, j) of dx [*, H, W, K],
+  // the gather reads dy [*, Ho, Wo, C] at (n, i + di, j + dj) for the class's taps
+  int ph = 0, pw = 0;
   // wgrad1x1 only: dy channels [k1, K) come from dy2 ([M, K - k1], output rows) — the BN
   // fold's dz^T x and Gram x^T x in one pass over x (k1 = K: single source)
   const __bf16* dy2 = nullptr;
@@ -76,7 +80,7 @@ struct RowInfo {
   uint32_t valid[A_CH];
 };
 
-template <int A_CH, int NT>
+template <int A_CH, int NT, bool DG = false>
 __device__ __forceinline__ void row_info(const Geo& g, const __bf16* X, int64_t m0, int tid,
                                          int sc, RowInfo<A_CH>& ri) {
 #pragma unroll
@@ -84,7 +88,15 @@ __device__ __forceinline__ void row_info(const Geo& g, const __bf16* X, int64_t 
     const int64_t m = m0 + i * (NT / 8) + (tid >> 3);
     ri.valid[i] = 0;
     ri.addr[i] = 0;
-    if (m < g.M) {
+    if (DG && m < g.M) {
+      // class row (n, ci, cj) reads dy (n, ci + di, cj + dj): bit 2 di + dj when inside dy
+      const int hw = g.Ho * g.Wo;
+      const int rem = (int)(m % hw);
+      const int ci = rem / g.Wo, cj = rem - ci * g.Wo;
+      const bool r1 = ci + 1 < g.Ho, c1 = cj + 1 < g.Wo;
+      ri.valid[i] = 1u | (c1 ? 2u : 0u) | (r1 ? 4u : 0u) | (r1 && c1 ? 8u : 0u);
+      ri.addr[i] = (uint64_t)(X + (m * g.C + sc * 8));
+    } else if (m < g.M) {
       const int64_t hw = (int64_t)g.Ho * g.Wo;
       const int n = (int)(m / hw);
       const int rem = (int)(m - (int64_t)n * hw);
@@ -123,7 +135,7 @@ __device__ __forceinline__ void raw_barrier() {
 // sum d (x_bn - mean)) — mv_bn.hip's bwd_reduce_kernel<1> folded into the epilogue.
 // the second launch bound asks for 2 resident workgroups (the LDS ring allows 2): the
 // 8-wave BN-reduce variant otherwise grows past 128 VGPRs and runs one workgroup per CU
-template <int BM, int BN, int WM, int WN, int EPI, int NS = 3>
+template <int BM, int BN, int WM, int WN, int EPI, int NS = 3, bool DG = false>
 __global__ __launch_bounds__(WM * WN * 64)
 __attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void conv3x3_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Wt, __bf16* __restrict__ Y, Geo g,
@@ -149,7 +161,7 @@ __attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void con
   const int64_t stream = t / ntn, nstreams = gridDim.x / ntn;
   const int n0 = nt * BN;
   const int taps = g.ks * g.ks;
-  const int csteps = g.C / BK, KT = taps * csteps;
+  const int csteps = g.C / BK, KT = (DG ? (1 + g.ph) * (1 + g.pw) : taps) * csteps;
   const int64_t wrow = (int64_t)taps * g.C;       // filter row length
   const int sc = (tid & 7) ^ ((tid >> 3) & 7);    // swizzled source chunk of this thread
 
@@ -160,10 +172,21 @@ __attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void con
   const uint64_t zaddr = (uint64_t)(g_zero + (tid & 7) * 4);
 
   auto issue = [&](const RowInfo<A_CH>& ri, int kt, int buf) {
-    const int tap = kt / csteps, c0 = (kt - tap * csteps) * BK;   // wave-uniform
-    const int r = tap / g.ks, s = tap - r * g.ks;
-    const int64_t offa = (((int64_t)r * g.W + s) * g.C + c0) * 2;
-    const int64_t offb = ((int64_t)tap * g.C + c0) * 2;
+    int tap = kt / csteps;
+    const int c0 = (kt - tap * csteps) * BK;   // wave-uniform
+    int64_t offa, offb;
+    if constexpr (DG) {
+      // class tap t: dy row + tR, column + tS; flipped-filter tap (ph ? 2 tR : 1, pw ? 2 tS : 1)
+      const int tR = g.pw ? tap >> 1 : tap, tS = g.pw ? tap & 1 : 0;
+      const int rr = g.ph ? 2 * tR : 1, ss = g.pw ? 2 * tS : 1;
+      offa = (((int64_t)tR * g.Wo + tS) * g.C + c0) * 2;
+      offb = ((int64_t)(rr * 3 + ss) * g.C + c0) * 2;
+      tap = 2 * tR + tS;                     // validity bit
+    } else {
+      const int r = tap / g.ks, s = tap - r * g.ks;
+      offa = (((int64_t)r * g.W + s) * g.C + c0) * 2;
+      offb = ((int64_t)tap * g.C + c0) * 2;
+    }
     __bf16* As = smem + buf * STAGE;
     __bf16* Bs = As + BM * BK;
 #pragma unroll
@@ -203,7 +226,7 @@ __attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void con
   int64_t mt = stream;
   if (mt < ntm) {
     RowInfo<A_CH> iri;
-    row_info<A_CH, NT>(g, X, mt * BM, tid, sc, iri);
+    row_info<A_CH, NT, DG>(g, X, mt * BM, tid, sc, iri);
     int64_t imt = mt;          // (tile, step) of the last issued stage
     int ikt = 0;
     int islot = 0;
@@ -213,7 +236,7 @@ __attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void con
       int64_t m2 = imt;
       if (k2 == KT) { k2 = 0; m2 += nstreams; }
       if (m2 >= ntm) return false;
-      if (m2 != imt) row_info<A_CH, NT>(g, X, m2 * BM, tid, sc, iri);
+      if (m2 != imt) row_info<A_CH, NT, DG>(g, X, m2 * BM, tid, sc, iri);
       islot = islot + 1 == NS ? 0 : islot + 1;
       issue(iri, k2, islot);
       imt = m2;
@@ -254,8 +277,14 @@ __attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void con
       const int64_t m0 = mt * BM;
 #pragma unroll
       for (int b = 0; b < TM; ++b) {
-        const int64_t row = m0 + wm * WTM + b * 16 + rl;
+        int64_t row = m0 + wm * WTM + b * 16 + rl;
         if (row < g.M) {
+          if constexpr (DG) {          // class row -> dx pixel (n, 2 ci + ph, 2 cj + pw)
+            const uint32_t hw = (uint32_t)(g.Ho * g.Wo), r32 = (uint32_t)row;
+            const uint32_t n = r32 / hw, rem = r32 - n * hw;
+            const uint32_t ci = rem / (uint32_t)g.Wo, cj = rem - ci * (uint32_t)g.Wo;
+            row = ((int64_t)n * g.H + 2 * ci + g.ph) * g.W + 2 * cj + g.pw;
+          }
 #pragma unroll
           for (int a = 0; a < TN; ++a) {
             const f32x4v v = acc[a][b];
@@ -470,6 +499,54 @@ bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, in
     if (partial) MV_LAUNCH(64, true) else MV_LAUNCH(64, false)
   }
 #undef MV_LAUNCH
+  return true;
+}
+
+// Stride-2 3x3 (pad 1) data gradient: dx [Nb, H, W, C] from dy [Nb, H/2, W/2, K] and the
+// transposed flipped filter wt [C][3][3][K]; four parity-class launches (DG), every dx pixel
+// written once.  C % 256 == 0 goes to mv_gemm256.hip's AMODE 4, else conv3x3_kernel.
+bool mv_conv3x3_s2_dgrad_supported(int Nb, int H, int W, int C, int K) {
+  if (mv_dgrad256_s2_supported(Nb, H, W, C, K)) return true;
+  return Nb > 0 && H >= 2 && W >= 2 && !(H & 1) && !(W & 1) && C % 64 == 0 && K % 64 == 0 &&
+         C > 0 && K > 0 && (int64_t)Nb * H * W * std::max(C, K) < (int64_t(1) << 40);
+}
+
+bool mv_conv3x3_s2_dgrad(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C,
+                         int K, hipStream_t st) {
+  using namespace mv::conv;
+  if (mv_dgrad256_s2_supported(Nb, H, W, C, K))
+    return mv_dgrad256_s2(dy, wt, dx, Nb, H, W, C, K, nullptr, nullptr, nullptr, st);
+  if (!mv_conv3x3_s2_dgrad_supported(Nb, H, W, C, K)) return false;
+  Geo g;
+  g.ks = 3;
+  g.st = 2;
+  g.H = H;
+  g.W = W;
+  g.C = K;             // gathered (dy) channels
+  g.K = C;             // output (dx) channels
+  g.Ho = H / 2;
+  g.Wo = W / 2;
+  g.M = (int64_t)Nb * g.Ho * g.Wo;
+  const __bf16* X = (const __bf16*)dy;
+  const __bf16* Wt = (const __bf16*)wt;
+  __bf16* Y = (__bf16*)dx;
+#define MV_LAUNCH_DG(BNV)                                                                      \
+  {                                                                                            \
+    constexpr int BMV = Cfg<BNV, false>::BM, WMV = Cfg<BNV, false>::WM;                        \
+    constexpr int WNV = Cfg<BNV, false>::WN, NSV = Cfg<BNV, false>::NS;                        \
+    const int64_t ntm = (g.M + BMV - 1) / BMV;                                                 \
+    const int ntn = C / BNV;                                                                   \
+    const int64_t ns = streams_for<BNV, false>(ntm, ntn);                                      \
+    hipLaunchKernelGGL((conv3x3_kernel<BMV, BNV, WMV, WNV, 0, NSV, true>),                      \
+                       dim3((unsigned)(ns * ntn)), dim3(WMV * WNV * 64), 0, st, X, Wt, Y, g, ntn, \
+                       ntm, nullptr, nullptr, nullptr, nullptr);                               \
+  }
+  for (int c = 3; c >= 0; --c) {      // the 4-tap class first
+    g.ph = c >> 1;
+    g.pw = c & 1;
+    if (conv_bn_of(C) == 128) MV_LAUNCH_DG(128) else MV_LAUNCH_DG(64)
+  }
+#undef MV_LAUNCH_DG
   return true;
 }
 

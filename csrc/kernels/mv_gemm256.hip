@@ -82,6 +82,13 @@ __device__ __forceinline__ void barrier() {
 // tap kt / (Cin / 64); each staged row carries its tap-(0, 0) address and a 9-bit mask of
 // the taps inside the image (padding taps read a zero page); B = the [N][ks][ks][Cin]
 // filter, already K-contiguous.
+// 4 stride-2 3x3 (pad 1) DATA gradient, one output parity class (ph, pw) per launch: dx
+// pixel (n, 2i + ph, 2j + pw) only receives the taps r' = 1 (ph = 0) or r' in {0, 2}
+// (ph = 1) of the flipped filter (columns likewise), reading dy (n, i + r'/2, j + s'/2) —
+// a gather GEMM over the class's 1, 2 or 4 taps (K = taps x Cin, dy channels) with no
+// structurally-zero products and no zero-filled dx (every dx pixel is in one class).
+// A = dy [*, Ho, Wo, Cin]; B = the transposed, flipped filter [N][3][3][Cin] (row Kb =
+// 9 Cin); M = Nb Ho Wo class rows, stored at dx row (n, 2i + ph, 2j + pw) of [*, H, W, N].
 // Epilogues: 0 plain; 1 + BN statistics of the bf16 C around shift; 4 the BN fold's data
 // gradient (mv_gemm.hip EPI 4): C + badd (badd may be null: the 3x3 data gradient with the
 // producing BN+ReLU's backward reduce, mv_conv.hip EPI 2), d = fma(xb, sc, bi) > 0 ? bf16 : 0
@@ -96,6 +103,7 @@ struct Args {
   int64_t ntiles;
   int ds, H, W, Ho, Wo;
   int Cin, ks;                    // AMODE 3
+  int ph, pw, Kb;                 // AMODE 4: parity class, filter row length (9 Cin)
   const float* shift;
   float* partial;
   const float* badd;
@@ -150,7 +158,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   uint32_t avalid[2];              // AMODE 3: taps inside the image, row i at bit 16 i
   const uint32_t scb = (uint32_t)(((lane & 7) ^ ((lane >> 3) & 7)) * 16);   // = sc * 16 bytes
   const int KT = p.K / BK, KT1 = AMODE == 2 ? p.K1 / BK : KT;
-  const int csteps = AMODE == 3 ? p.Cin / BK : 1;
+  const int csteps = (AMODE == 3 || AMODE == 4) ? p.Cin / BK : 1;
   auto set_src = [&](int64_t tl) {
     const int64_t mt = tl / p.ntn;
     const int nt = (int)(tl - mt * p.ntn);
@@ -192,19 +200,31 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
           abase[h][i] =
               (uint32_t)(((((int64_t)n * p.H + hi0) * p.W + wi0) * p.Cin + sc * 8) * 2);
         }
+        if constexpr (AMODE == 4) {
+          // class row (n, ci, cj) reads dy (n, ci + di, cj + dj), di, dj in {0, 1}: bit
+          // 2 di + dj set when that pixel is inside dy
+          const int hw = p.Ho * p.Wo;
+          const int rem = (int)(row % hw);
+          const int ci = rem / p.Wo, cj = rem - ci * p.Wo;
+          const bool r1 = ci + 1 < p.Ho, c1 = cj + 1 < p.Wo;
+          const uint32_t v = 1u | (c1 ? 2u : 0u) | (r1 ? 4u : 0u) | (r1 && c1 ? 8u : 0u);
+          if (i == 0) avalid[h] = v;
+          else avalid[h] |= v << 16;
+          abase[h][i] = (uint32_t)((row * p.Cin + sc * 8) * 2);
+        }
         if constexpr (AMODE == 2) {
           offa[h][i] = (uint32_t)row;
         } else {
           offa[h][i] = (uint32_t)((row * p.K + sc * 8) * 2);
         }
         const int col = nt * BN + (r >> 5) * 64 + h * 32 + (r & 31);
-        offb[h][i] = (uint32_t)(((int64_t)col * p.K + sc * 8) * 2);
+        offb[h][i] = (uint32_t)(((int64_t)col * (AMODE == 4 ? p.Kb : p.K) + sc * 8) * 2);
       }
     }
   };
   auto issue = [&](int slot, int buf, int kt) {
     // AMODE 3: the K tile's filter tap and channel block (wave-uniform)
-    uint32_t toff = 0;
+    uint32_t toff = 0, boff = kt * (BK * 2);
     int tap = 0;
     if constexpr (AMODE == 3) {
       tap = kt / csteps;
@@ -212,12 +232,22 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
       const int tr = tap / p.ks, ts = tap - tr * p.ks;
       toff = (uint32_t)(((tr * p.W + ts) * p.Cin + c0) * 2);
     }
+    if constexpr (AMODE == 4) {
+      // class tap t: row tap r' = ph ? 2 tR : 1 (dy row + tR), column s' = pw ? 2 tS : 1
+      const int t = kt / csteps;
+      const int c0 = (kt - t * csteps) * BK;
+      const int tR = p.pw ? t >> 1 : t, tS = p.pw ? t & 1 : 0;
+      const int rr = p.ph ? 2 * tR : 1, ss = p.pw ? 2 * tS : 1;
+      tap = 2 * tR + tS;                                   // the validity bit of (di, dj)
+      toff = (uint32_t)(((tR * p.Wo + tS) * p.Cin + c0) * 2);
+      boff = (uint32_t)(((rr * 3 + ss) * p.Cin + c0) * 2);
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const char* src;
       if (slot >= 2) {
-        src = reinterpret_cast<const char*>(p.B) + offb[slot - 2][i] + kt * (BK * 2);
-      } else if (AMODE == 3) {
+        src = reinterpret_cast<const char*>(p.B) + offb[slot - 2][i] + boff;
+      } else if (AMODE == 3 || AMODE == 4) {
         // (padding taps: every lane reads the same zero chunk — the DMA writes lane * 16)
         src = ((avalid[slot] >> (tap + 16 * i)) & 1u)
                   ? reinterpret_cast<const char*>(p.A) + (uint32_t)(abase[slot][i] + toff)
@@ -280,6 +310,17 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   // holds 8 consecutive channels of its row — g = 0 / 2: tile 2q columns 0-7 / 8-15,
   // g = 1 / 3: tile 2q + 1 columns 0-7 / 8-15 (half the store instructions of the
   // fragment layout's 8-byte stores, 64-B row segments instead of 32-B).
+  // C / xb row of GEMM row `row` (AMODE 4: the class pixel (n, 2i + ph, 2j + pw) of dx)
+  auto out_row = [&](int64_t row) -> int64_t {
+    if constexpr (AMODE != 4) {
+      return row;
+    } else {
+      const uint32_t hw = (uint32_t)(p.Ho * p.Wo), r32 = (uint32_t)row;
+      const uint32_t n = r32 / hw, rem = r32 - n * hw;
+      const uint32_t ci = rem / (uint32_t)p.Wo, cj = rem - ci * (uint32_t)p.Wo;
+      return ((int64_t)n * p.H + 2 * ci + p.ph) * p.W + 2 * cj + p.pw;
+    }
+  };
   auto epilogue = [&](int64_t tl) {
     const int64_t mt = tl / p.ntn;
     const int n0 = (int)(tl - mt * p.ntn) * BN;
@@ -303,16 +344,18 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
           const int64_t row = m0 + wm * (MT * 16) + (b + bb) * 16 + rl;
+          const int64_t orow = out_row(row);
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int c0 = n0 + wn * 64 + q * 32 + (g & 1) * 16 + (g >> 1) * 8;
-            xr[bb][q] = (b + bb < MT && row < p.M) ? *reinterpret_cast<const uint4*>(p.xb + row * N + c0)
+            xr[bb][q] = (b + bb < MT && row < p.M) ? *reinterpret_cast<const uint4*>(p.xb + orow * N + c0)
                                   : uint4{0u, 0u, 0u, 0u};
           }
         }
       }
       const int64_t row = m0 + wm * (MT * 16) + b * 16 + rl;
       const bool in = row < p.M;
+      const int64_t orow = out_row(row);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         f32x4v u = acc[2 * q][b], v = acc[2 * q + 1][b];
@@ -364,7 +407,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
           }
         }
         if (in && (EPI != 1 || p.C))        // EPI 1 with C == null: statistics only
-          *reinterpret_cast<uint4*>(p.C + row * N + c0) = uint4{o[0], o[1], o[2], o[3]};
+          *reinterpret_cast<uint4*>(p.C + orow * N + c0) = uint4{o[0], o[1], o[2], o[3]};
       }
     }
     if constexpr (STATS) {
@@ -890,6 +933,61 @@ bool mv_conv256(const void* X, const void* Wt, void* Y, int Nb, int H, int W, in
     g256_launch<1, 3>(a, st);
   } else {
     g256_launch<0, 3>(a, st);
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------- stride-2 3x3 data gradient
+// (AMODE 4): four launches, one per output parity class, each a gather GEMM over that
+// class's taps.  Cin = dx channels (the GEMM's N), Cout = dy channels.
+bool mv_dgrad256_s2_supported(int Nb, int H, int W, int Cin, int Cout) {
+  if (Nb < 1 || H < 2 || W < 2 || (H & 1) || (W & 1)) return false;
+  const int64_t M = (int64_t)Nb * (H / 2) * (W / 2);
+  return Cin % 256 == 0 && Cin <= mv::g256::kVecFloats / 4 && Cout % 64 == 0 && Cout > 0 &&
+         M * Cout * 2 < (int64_t(1) << 32) && (M + 255) / 256 * (Cin / 256) < (int64_t(1) << 31) &&
+         (int64_t)Cin * 9 * Cout * 2 < (int64_t(1) << 32) && M * 4 < (int64_t(1) << 31);
+}
+
+int64_t mv_dgrad256_s2_partials(int Nb, int H, int W, int Cin) {
+  return 4 * mv_gemm256_partials((int64_t)Nb * (H / 2) * (W / 2), Cin);
+}
+
+bool mv_dgrad256_s2(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int Cin,
+                    int Cout, float* partial, const void* bn_x, const float* bn_vec,
+                    hipStream_t st) {
+  using namespace mv::g256;
+  if (!mv_dgrad256_s2_supported(Nb, H, W, Cin, Cout) || (bn_x && !partial) ||
+      (!bn_x && partial))
+    return false;
+  Args a{};
+  a.A = (const __bf16*)dy;
+  a.B = (const __bf16*)wt;
+  a.C = (__bf16*)dx;
+  a.H = H;
+  a.W = W;
+  a.Ho = H / 2;
+  a.Wo = W / 2;
+  a.M = (int64_t)Nb * a.Ho * a.Wo;
+  a.N = Cin;
+  a.Cin = Cout;
+  a.Kb = 9 * Cout;
+  a.ds = 2;
+  const int64_t prow = mv_gemm256_partials(a.M, Cin);
+  // the 4-tap class first: the later, shorter launches fill in behind it
+  for (int c = 3; c >= 0; --c) {
+    a.ph = c >> 1;
+    a.pw = c & 1;
+    a.K = (1 + a.ph) * (1 + a.pw) * Cout;
+    if (bn_x) {
+      a.xb = (const __bf16*)bn_x;
+      a.mean = bn_vec;
+      a.sc = bn_vec + 2 * Cin;
+      a.bi = bn_vec + 3 * Cin;
+      a.partial = partial + (int64_t)(3 - c) * prow * 2 * Cin;
+      g256_launch<4, 4>(a, st);
+    } else {
+      g256_launch<0, 4>(a, st);
+    }
   }
   return true;
 }

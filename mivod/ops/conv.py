@@ -273,6 +273,24 @@ def _dgrad_on_mivod(cin: int, cout: int) -> bool:
     return max(cin, cout) <= int(v)
 
 
+def _dgrad_s2_on_mivod(cin: int, h: int, w: int) -> bool:
+    """Stride-2 data gradient as four output-parity-class gather GEMMs (mv_gemm256.hip AMODE
+    4 for dx channels % 256 == 0, mv_conv.hip's conv3x3_kernel DG mode otherwise; even input
+    H, W) instead of MIOpen's backward-data solver plus its zero fill (scripts/
+    micro_dgrad_s2.py, bs2048: layer3 1087 -> 683 us, layer4 1038 -> 644 us).
+    MIVOD_CONV3X3_DGRAD_S2=0 disables it."""
+    return (os.environ.get("MIVOD_CONV3X3_DGRAD_S2", "1") != "0" and cin % 64 == 0
+            and h % 2 == 0 and w % 2 == 0)
+
+
+def _dgrad_s2_bn(cin: int) -> bool:
+    """The producing BN+ReLU's backward reduce in the stride-2 data gradient's epilogue
+    (256 x 256 pipeline only).  Off by default: the epilogue's scattered BN-input reads are
+    latency-bound (micro: layer3 683 -> 1081 us, more than the separate reduce pass's
+    241 us); MIVOD_CONV3X3_DGRAD_S2_BN=1 turns it on."""
+    return os.environ.get("MIVOD_CONV3X3_DGRAD_S2_BN", "0") == "1" and cin % 256 == 0
+
+
 def _wgrad_on_mivod(cin: int, cout: int, stride: int) -> bool:
     """mivod's 3x3 weight-gradient kernel (csrc/kernels/mv_conv.hip wgrad3x3_kernel) beats
     MIOpen's on every ResNet-50 conv2 shape except the 512-channel stride-2 one
@@ -294,7 +312,8 @@ class _Conv3x3(torch.autograd.Function):
     output of a fused BN+ReLU (``slot``, mode 1), mivod's kernel also runs that BN's
     backward reduce in its epilogue and hands (d, partials) to it through the slot, the
     same protocol as ``_Conv1x1BN``; the weight gradient on mivod's wgrad3x3 kernel
-    (MIOpen for the 512-channel stride-2 conv); stride-2 data gradient from MIOpen."""
+    (MIOpen for the 512-channel stride-2 conv); stride-2 data gradient on mv_gemm256's
+    parity-class GEMMs (even input size; optionally with the BN+ReLU reduce), else MIOpen."""
 
     @staticmethod
     def forward(ctx, x, w, stride, shift, stats, slot):
@@ -344,7 +363,21 @@ class _Conv3x3(torch.autograd.Function):
                 else:
                     dx = F.conv2d(dy, wt, None, 1, 1)
         else:
-            if need_x:
+            r = []
+            if need_x and s == 2 and _dgrad_s2_on_mivod(w.shape[1], x.shape[2], x.shape[3]):
+                from . import kernels as K
+                wt = _transposed_filter(w)
+                if (slot is not None and slot.bn is not None and slot.mode == 1
+                        and slot.pending is None):
+                    xb, _, vec = slot.bn
+                    r = K.native().conv3x3_s2_dgrad(dy, wt, x.shape[2], x.shape[3], xb, vec)
+                    if r:
+                        slot.pending = (r[0], r[1])
+                else:
+                    r = K.native().conv3x3_s2_dgrad(dy, wt, x.shape[2], x.shape[3])
+                    if r:
+                        dx = r[0]
+            if need_x and not r:
                 dx, _, _ = torch.ops.aten.convolution_backward(
                     dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])
         if need_w:
@@ -358,16 +391,21 @@ class _Conv3x3(torch.autograd.Function):
 
 
 def bwd3x3_fusable(m: nn.Conv2d, x: torch.Tensor):
-    """GradSlot of x's producer when this stride-1 3x3 conv's data gradient runs on
-    mivod's kernel and can carry that producer's BN+ReLU backward reduce; else None."""
+    """GradSlot of x's producer when this 3x3 conv's data gradient runs on mivod's kernel
+    (stride 1, or stride 2 on the parity-class GEMMs) and can carry that producer's
+    BN+ReLU backward reduce; else None."""
     slot = getattr(x, "_mv_slot", None)
     if (slot is None or getattr(slot, "bn", None) is None or getattr(slot, "mode", 0) != 1
             or os.environ.get("MIVOD_CONV_BN_BWD_FUSE", "1") == "0"
             or os.environ.get("MIVOD_CONV3X3_BN_BWD", "1") == "0"
-            or not (torch.is_grad_enabled() and x.requires_grad) or m.stride[0] != 1
-            or not _dgrad_on_mivod(m.in_channels, m.out_channels)):
+            or not (torch.is_grad_enabled() and x.requires_grad)):
         return None
-    return slot
+    if m.stride[0] == 1 and _dgrad_on_mivod(m.in_channels, m.out_channels):
+        return slot
+    if (m.stride[0] == 2 and _dgrad_s2_on_mivod(m.in_channels, x.shape[2], x.shape[3])
+            and _dgrad_s2_bn(m.in_channels)):
+        return slot
+    return None
 
 
 def conv3x3_bn(m: nn.Conv2d, x: torch.Tensor, shift, stats: bool, slot=None):
