@@ -462,6 +462,27 @@ at::Tensor bn_stats(at::Tensor x, c10::optional<at::Tensor> gamma, c10::optional
   return vec;
 }
 
+// statistics of x[:, :, ::s, ::s] without the strided copy -> [4, C] {mean, invstd, ...}
+at::Tensor bn_stats_strided(at::Tensor x, int64_t stride) {
+  int64_t C;
+  bn_check_act(x, "x", &C);
+  TORCH_CHECK(stride >= 1 && stride < 65536 && x.size(2) < 65536 && x.size(3) < 65536,
+              "bn_stats_strided: bad stride / size");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t M = N * ((H - 1) / stride + 1) * ((W - 1) / stride + 1);
+  TORCH_CHECK(M > 0 && M < (int64_t(1) << 32), "bn_stats_strided: empty or too large");
+  c10::DeviceGuard guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  const int P = mv_bn_partials(M, (int)C);
+  at::Tensor partial = at::empty({(int64_t)P * 2 * C}, fo);
+  at::Tensor vec = at::empty({4, C}, fo);
+  mv_bn_stats_strided(x.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)stride,
+                      partial.data_ptr<float>(), P, vec[0].data_ptr<float>(),
+                      vec[1].data_ptr<float>(), vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
+                      cur_stream());
+  return vec;
+}
+
 // returns {dx, dgamma, dbeta, dz}; dz defined only for modes 2 and 3 (residual branch grad)
 std::vector<at::Tensor> bn_bwd(int64_t mode, at::Tensor dy, at::Tensor x,
                                c10::optional<at::Tensor> y, at::Tensor vec,
@@ -1005,6 +1026,34 @@ at::Tensor gemm_fold_dx(at::Tensor a1, at::Tensor a2, at::Tensor b, at::Tensor b
 }
 
 bool gemm_dual_supported(int64_t K1, int64_t K2) { return mv_gemm_dual_supported((int)K1, (int)K2); }
+
+// D [M, N] = [A1 | x[:, :, ::s, ::s]] . B^T + badd on the 256 x 256 pipeline with the second
+// source gathered from the channels_last x [Nb, K2, H, W] (no strided copy); false when the
+// shape is not covered (N % 256 or the K splits)
+bool gemm_dual_bias_strided(at::Tensor a1, at::Tensor x, int64_t stride, at::Tensor b,
+                            at::Tensor badd, at::Tensor d) {
+  for (const at::Tensor* t : {&a1, &b, &d})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 2 &&
+                    t->is_contiguous() && t->device() == a1.device(),
+                "gemm_dual_bias_strided: A1, B, D must be contiguous 2-D bf16 tensors on one GPU");
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.device() == a1.device(),
+              "gemm_dual_bias_strided: x must be a channels_last bf16 [Nb, K2, H, W] tensor");
+  TORCH_CHECK(stride >= 1 && stride < 65536 && x.size(2) < 65536 && x.size(3) < 65536,
+              "gemm_dual_bias_strided: bad stride / size");
+  const int64_t M = a1.size(0), K1 = a1.size(1), K2 = x.size(1), N = b.size(0);
+  const int64_t H = x.size(2), W = x.size(3);
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  TORCH_CHECK(M == x.size(0) * Ho * Wo && b.size(1) == K1 + K2 && d.size(0) == M &&
+                  d.size(1) == N, "gemm_dual_bias_strided: shape mismatch");
+  TORCH_CHECK(badd.is_cuda() && badd.scalar_type() == at::kFloat && badd.is_contiguous() &&
+                  badd.numel() == N && badd.device() == a1.device(),
+              "gemm_dual_bias_strided: badd must be fp32 [N]");
+  c10::DeviceGuard guard(a1.device());
+  return mv_gemm256_dual(a1.data_ptr(), x.data_ptr(), b.data_ptr(), badd.data_ptr<float>(),
+                         d.data_ptr(), M, (int)K1, (int)K2, (int)N, nullptr, nullptr, nullptr,
+                         nullptr, nullptr, cur_stream(), (int)stride, (int)H, (int)W);
+}
 
 // d = [a1 | a2] . b^T + badd (bf16 [M, K2])
 void gemm_dual_bias(at::Tensor a1, at::Tensor a2, at::Tensor b, at::Tensor badd, at::Tensor d) {
@@ -1561,12 +1610,18 @@ at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride, bool fp32_out,
   // dy2: a second dy stream stacked below dy's channels (dw = [dy | dy2]^T . x)
   const bool two = dy2.has_value() && dy2->defined();
   int64_t K = K1;
+  bool gather = false;
   if (two) {
+    // [N, K2, Ho, Wo] at the output rows, or (stride 2) [N, K2, H, W] read at each output
+    // row's strided input pixel (e.g. dy2 = x itself: the Gram pass of x[:, :, ::2, ::2])
+    gather = stride > 1 && dy2->dim() == 4 && dy2->size(2) == H && dy2->size(3) == W;
     TORCH_CHECK(dy2->is_cuda() && dy2->scalar_type() == at::kBFloat16 && dy2->dim() == 4 &&
                     dy2->is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                    dy2->device() == x.device() && dy2->size(0) == N && dy2->size(2) == Ho &&
-                    dy2->size(3) == Wo && dy2->size(1) % 64 == 0,
-                "wgrad1x1: dy2 must be a channels_last bf16 [N, K2, Ho, Wo] tensor");
+                    dy2->device() == x.device() && dy2->size(0) == N &&
+                    (gather || (dy2->size(2) == Ho && dy2->size(3) == Wo)) &&
+                    dy2->size(1) % 64 == 0,
+                "wgrad1x1: dy2 must be a channels_last bf16 [N, K2, Ho, Wo] (or, stride 2, "
+                "[N, K2, H, W]) tensor");
     K = K1 + dy2->size(1);
   }
   TORCH_CHECK(C % 64 == 0 && K % 64 == 0 && N * H * W * std::max(C, K) < (int64_t(1) << 40),
@@ -1579,7 +1634,7 @@ at::Tensor wgrad1x1(at::Tensor x, at::Tensor dy, int64_t stride, bool fp32_out,
                             at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(mv_wgrad1x1(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), work.data_ptr<float>(),
                           (int)N, (int)H, (int)W, (int)C, (int)K, (int)stride, cur_stream(),
-                          fp32_out, two ? dy2->data_ptr() : nullptr, (int)K1),
+                          fp32_out, two ? dy2->data_ptr() : nullptr, (int)K1, gather),
               "wgrad1x1: unsupported shape");
   return dw;
 }
@@ -1631,6 +1686,8 @@ PYBIND11_MODULE(_mvk, m) {
         "fused BN(+add)(+ReLU) forward from the conv epilogue's statistics partials");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BN(+add)(+ReLU) backward (+ second grad stream)");
   m.def("bn_stats", &bn_stats, "NHWC BN training statistics only -> [4, C]");
+  m.def("bn_stats_strided", &bn_stats_strided,
+        "statistics of x[:, :, ::s, ::s] (no strided copy) -> [4, C] {mean, invstd, ...}");
   m.def("bn_apply_colsum", &bn_apply_colsum,
         "{y, [P, C] partials}: relu(x*scale + bias) with column sums of y");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC maxpool with fused affine+ReLU prologue -> (y, idx)");
@@ -1656,6 +1713,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_nt_apply_dual", &gemm_nt_apply_dual,
         "{y, mask}: the BN+add+ReLU apply GEMM with the shortcut conv + BN recomputed inside");
   m.def("gemm_dual_supported", &gemm_dual_supported, "gemm_dual_bias handles (K1, K2)");
+  m.def("gemm_dual_bias_strided", &gemm_dual_bias_strided,
+        "[A1 | x[:, :, ::s, ::s]] . B^T + badd without the strided copy; False if not covered");
   m.def("gemm_dual_bias", &gemm_dual_bias, "d = [a1 | a2] . b^T + badd (dual-source MFMA GEMM)");
   m.def("gemm_fold_dx_partials", &gemm_fold_dx_partials,
         "partial rows of gemm_fold_dx for (M, K1, K2) (-1: unsupported)");

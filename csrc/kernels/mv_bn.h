@@ -44,3 +44,10 @@ void mv_bn_bwd(int mode, const void* dy, const void* dy2, const void* x, const v
 // <= mv_bn_partials(M, C))
 int mv_bn_apply_colsum(const void* x, void* y, int64_t M, int C, const float* scale,
                        const float* bias, float* partial, hipStream_t st);
+
+// statistics of the stride-ds grid rows of x [Nb, H, W, C] (what a stride-ds 1x1 conv reads):
+// saved {mean, invstd, scale, bias} with gamma = 1, beta = 0; partial: [P][2][C] workspace,
+// P = mv_bn_partials(rows, C)
+void mv_bn_stats_strided(const void* x, int Nb, int H, int W, int C, int ds, float* partial,
+                         int P, float* save_mean, float* save_invstd, float* scale, float* bias,
+                         hipStream_t st);

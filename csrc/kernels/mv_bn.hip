@@ -38,7 +38,18 @@ struct Geo {
   int TPR;   // lanes per row
   int RPI;   // rows per iteration (per workgroup)
   int64_t RB;  // rows per workgroup
+  // stats_kernel only: ds > 1 reads row r of the stride-ds grid of a [*, H, W, C] input
+  // (the rows a stride-ds 1x1 conv reads) instead of row r of x
+  int ds = 1, H = 1, W = 1;
 };
+
+__device__ __forceinline__ int64_t src_row(const Geo& g, int64_t r) {
+  if (g.ds == 1) return r;
+  const uint32_t Ho = (uint32_t)((g.H - 1) / g.ds + 1), Wo = (uint32_t)((g.W - 1) / g.ds + 1);
+  const uint32_t r32 = (uint32_t)r, t = r32 / Wo, wo = r32 - t * Wo;
+  const uint32_t n = t / Ho, ho = t - n * Ho;
+  return ((int64_t)n * g.H + ho * g.ds) * g.W + wo * g.ds;
+}
 
 __device__ __forceinline__ void lane_map(const Geo& g, int* tc, int* tr, int* c, bool* valid) {
   *tc = threadIdx.x % g.TPR;
@@ -117,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(const __bf16* __restrict_
     for (; r + (U - 1) * g.RPI < r1; r += U * g.RPI) {
       float v[U][8];
 #pragma unroll
-      for (int u = 0; u < U; ++u) ldfirst<RNT>(x + (r + u * g.RPI) * g.C + c, v[u]);
+      for (int u = 0; u < U; ++u) ldfirst<RNT>(x + src_row(g, r + u * g.RPI) * g.C + c, v[u]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float a1 = 0.f, a2 = 0.f;
@@ -133,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void stats_kernel(const __bf16* __restrict_
     }
     for (; r < r1; r += g.RPI) {
       float v0[8];
-      ldfirst<RNT>(x + r * g.C + c, v0);
+      ldfirst<RNT>(x + src_row(g, r) * g.C + c, v0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float a = v0[j] - sh[j];
@@ -672,6 +683,24 @@ void mv_bn_fwd_train(const void* x, const void* res, void* y, int64_t M, int C, 
                      partial, (int)grr.x, M, C, rmean, rvar, gamma, beta, momentum, eps, save_mean,
                      save_invstd, scale, bias);
   if (y) mv_bn_apply(x, res, y, M, C, scale, bias, relu, st, mask);   // y == null: statistics only
+}
+
+// Statistics (no running-stat update, no apply) of the rows a stride-ds 1x1 conv reads
+// from x [Nb, H, W, C]: mean / invstd over Nb * ceil(H/ds) * ceil(W/ds) rows, no strided copy
+void mv_bn_stats_strided(const void* x, int Nb, int H, int W, int C, int ds, float* partial,
+                         int P, float* save_mean, float* save_invstd, float* scale, float* bias,
+                         hipStream_t st) {
+  const int64_t M = (int64_t)Nb * ((H - 1) / ds + 1) * ((W - 1) / ds + 1);
+  Geo gr = reduce_geo(M, C, P, (const void*)&stats_kernel<8, true>);
+  gr.ds = ds;
+  gr.H = H;
+  gr.W = W;
+  const dim3 grr = grid_of(gr);
+  hipLaunchKernelGGL((stats_kernel<8, true>), grr, dim3(kBlock), 0, st, (const __bf16*)x,
+                     (const float*)nullptr, partial, gr);
+  hipLaunchKernelGGL(finalize_fwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kBlock), 0, st,
+                     partial, (int)grr.x, M, C, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f,
+                     save_mean, save_invstd, scale, bias);
 }
 
 // The statistics were produced elsewhere (the 1x1 conv GEMM's fused epilogue,

@@ -34,7 +34,9 @@ int64_t mv_wgrad1x1_workspace(int64_t M, int K, int C);
 // dy2 != null: dy's channels [k1, K) come from dy2 ([N, Ho, Wo, K - k1]) — dw = [dy | dy2]^T . x
 bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
                  int K, int stride, hipStream_t st, bool dw_fp32 = false,
-                 const void* dy2 = nullptr, int k1 = 0);
+                 const void* dy2 = nullptr, int k1 = 0, bool dy2_gather = false);
+// (dy2_gather: dy2 is [N, H, W, K - k1] at the input resolution, read at each output row's
+// strided input pixel — stride 2 only)
 
 // 64 -> 64 channel 3x3 / stride 1 "row patch" kernel (mv_conv64.hip): filter resident in
 // LDS, 8-row input patches staged once for all 9 taps.  W <= 62.  grid = persistent

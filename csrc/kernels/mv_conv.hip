@@ -69,6 +69,9 @@ struct Geo {
   // fold's dz^T x and Gram x^T x in one pass over x (k1 = K: single source)
   const __bf16* dy2 = nullptr;
   int k1 = 0;
+  // dy2x: dy2 is [*, H, W, K - k1] at the INPUT resolution, read at the strided pixel of
+  // each output row like X (the shortcut fold's Gram pass over x0[:, :, ::s, ::s])
+  int dy2x = 0;
 };
 
 // per-thread state of the A rows it stages (A_CH rows, fixed source chunk): the byte
@@ -879,7 +882,8 @@ __attribute__((amdgpu_waves_per_eu(FK == 2 ? 2 : 1))) void wgrad1x1_kernel(
       const void* src =
           r >= KS ? (const void*)(X + xrow[ws] * g.C + c0 + (r - KS) * 64 + sch * 8)
           : kk < g.k1 ? (const void*)(DY + mrow[ws] * g.k1 + kk + sch * 8)
-                      : (const void*)(g.dy2 + mrow[ws] * (g.K - g.k1) + (kk - g.k1) + sch * 8);
+                      : (const void*)(g.dy2 + (g.dy2x ? xrow[ws] : mrow[ws]) * (g.K - g.k1) +
+                                      (kk - g.k1) + sch * 8);
       glds16(in ? src : (const void*)zaddr, stg + j * WG_TILE);
     }
   };
@@ -1044,12 +1048,15 @@ int64_t mv_wgrad1x1_workspace(int64_t M, int K, int C) {
 }
 
 bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
-                 int K, int stride, hipStream_t st, bool dw_fp32, const void* dy2, int k1) {
+                 int K, int stride, hipStream_t st, bool dw_fp32, const void* dy2, int k1,
+                 bool dy2_gather) {
   using namespace mv::conv;
   if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2)) return false;
+  if (dy2_gather && (!dy2 || stride == 1)) return false;
   Geo g;
   g.dy2 = (const __bf16*)dy2;
   g.k1 = dy2 ? k1 : K;
+  g.dy2x = dy2_gather ? 1 : 0;
   if (dy2) {     // each staged k block must come from one source
     const W1Cfg c = w1_cfg(K, C);
     if (k1 <= 0 || k1 >= K || k1 % (64 * c.wk * c.fk) != 0) return false;

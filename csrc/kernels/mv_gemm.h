@@ -73,7 +73,9 @@ bool mv_gemm256_strided(const void* X, const void* B, void* C, int Nb, int H, in
 // (sum d, sum d (xb - mean)); without: plain store
 bool mv_gemm256_dual(const void* A1, const void* A2, const void* B, const float* badd, void* D,
                      int64_t M, int K1, int K2, int N, const void* xb, const float* mean,
-                     const float* scale, const float* bias, float* partial, hipStream_t st);
+                     const float* scale, const float* bias, float* partial, hipStream_t st,
+                     int ds = 1, int H = 0, int W = 0);
+// (ds > 1: A2 is [Nb, H, W, K2] read at each output row's stride-ds pixel — M = Nb Ho Wo)
 // 1x1 weight gradient on the 256 x 256 pipeline (stride 1): partial[S][K][C] fp32 with
 // S = mv_wgrad256_splits(M, C, K); DY channels [k1, K) from DY2 ([M, K - k1]) when k1 < K
 bool mv_wgrad256_supported(int64_t M, int C, int K, int k1);

@@ -152,6 +152,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   // columns {64 q + 32 h + j}.  Byte offsets at K offset 0 (the host checks < 4 GB).
   // (dual source: the A row index instead, both sources' offsets formed at issue)
   uint32_t offa[2][2], offb[2][2];
+  uint32_t offa2[2][2];            // AMODE 2: A2's row (the strided input row when ds > 1)
   uint32_t abase[2][2];            // AMODE 3: tap-(0, 0) byte offset of the row's chunk in
                                    // A (mod 2^32: negative at the top-left padding, only
                                    // used with a tap that lands inside the image)
@@ -214,6 +215,15 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
         }
         if constexpr (AMODE == 2) {
           offa[h][i] = (uint32_t)row;
+          int64_t row2 = row;
+          if (p.ds > 1) {          // A2 = x [*, H, W, K2] read at the output row's stride pixel
+            const int64_t hw = (int64_t)p.Ho * p.Wo;
+            const int64_t n = row / hw;
+            const int rem = (int)(row - n * hw);
+            const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+            row2 = (n * p.H + (int64_t)ho * p.ds) * p.W + (int64_t)wo * p.ds;
+          }
+          offa2[h][i] = (uint32_t)row2;
         } else {
           offa[h][i] = (uint32_t)((row * p.K + sc * 8) * 2);
         }
@@ -256,7 +266,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
         src = kt < KT1 ? reinterpret_cast<const char*>(p.A) + offa[slot][i] * (uint32_t)(p.K1 * 2) +
                              scb + kt * (BK * 2)
                        : reinterpret_cast<const char*>(p.A2) +
-                             offa[slot][i] * (uint32_t)((p.K - p.K1) * 2) + scb +
+                             (uint64_t)offa2[slot][i] * (uint32_t)((p.K - p.K1) * 2) + scb +
                              (kt - KT1) * (BK * 2);
       } else {
         src = reinterpret_cast<const char*>(p.A) + offa[slot][i] + kt * (BK * 2);
@@ -866,11 +876,22 @@ bool mv_gemm256_strided(const void* X, const void* B, void* C, int Nb, int H, in
 
 bool mv_gemm256_dual(const void* A1, const void* A2, const void* B, const float* badd, void* D,
                      int64_t M, int K1, int K2, int N, const void* xb, const float* mean,
-                     const float* scale, const float* bias, float* partial, hipStream_t st) {
+                     const float* scale, const float* bias, float* partial, hipStream_t st,
+                     int ds, int H, int W) {
   using namespace mv::g256;
   const int K = K1 + K2;
   if (K1 % 64 || K2 % 64 || !mv_gemm256_supported(M, N, K) || 4 * N > kVecFloats) return false;
   Args a{};
+  if (ds > 1) {       // A2 = [Nb, H, W, K2] read at the stride grid (M = Nb Ho Wo rows)
+    a.Ho = (H - 1) / ds + 1;
+    a.Wo = (W - 1) / ds + 1;
+    const int64_t hw = (int64_t)a.Ho * a.Wo;
+    if (H < 1 || W < 1 || M % hw != 0 || (M / hw) * H * W * (int64_t)K2 * 2 >= (int64_t(1) << 32))
+      return false;
+    a.ds = ds;
+    a.H = H;
+    a.W = W;
+  }
   a.A = (const __bf16*)A1;
   a.A2 = (const __bf16*)A2;
   a.B = (const __bf16*)B;

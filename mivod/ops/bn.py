@@ -699,32 +699,40 @@ class _Conv1x1BNFold(torch.autograd.Function):
             x0 = zr
             nb, c0 = x0.shape[0], x0.shape[1]
             cout_r = res_conv_w.shape[0]
-            x0s = x0 if s_r == 1 else _cl(x0[:, :, ::s_r, ::s_r])
-            ho, wo = x0s.shape[2], x0s.shape[3]
+            # x0s = x0[:, :, ::s, ::s] is never copied on the covered shapes: the kernels
+            # below read x0 at the stride grid (the copy is made lazily for the fallbacks)
+            x0s_c = [x0 if s_r == 1 else None]
+
+            def x0s():
+                if x0s_c[0] is None:
+                    x0s_c[0] = _cl(x0[:, :, ::s_r, ::s_r])
+                return x0s_c[0]
+            ho, wo = (x0.shape[2] - 1) // s_r + 1, (x0.shape[3] - 1) // s_r + 1
             mr = nb * ho * wo
             dzc = _cl(dz)
             need_wr = ctx.needs_input_grad[14]
-            if need_wr and _DUAL_WGRAD:      # [dz | x0s]^T . x0s (x0 read at the stride)
-                gg = nat.wgrad1x1(x0, dzc, s_r, True, x0s).view(cout_r + c0, c0)
+            if need_wr and _DUAL_WGRAD:      # [dz | x0s]^T . x0s (x0 read at the stride twice)
+                gg = nat.wgrad1x1(x0, dzc, s_r, True, x0).view(cout_r + c0, c0)
                 gr, gram = gg[:cout_r], gg[cout_r:]
             else:
                 gr = nat.wgrad1x1(x0, dzc, s_r, True).view(cout_r, c0)          # dz^T x0s
-                gram = nat.wgrad1x1(x0s, x0s, 1, True).view(c0, c0) if need_wr else None
+                gram = nat.wgrad1x1(x0s(), x0s(), 1, True).view(c0, c0) if need_wr else None
             # same dz as the main branch: its consumer's partials give sum dz
             part_r = fold_part
             sdz_r = None if part_r is not None else torch.sum(dzc, (0, 2, 3), dtype=torch.float32)
             dgr, dbr, dwrb, bcat, badd = _fold_math(
                 nat, res_conv_w.reshape(cout_r, c0), gr, gram, vec_r, res_w, mr, part_r, sdz_r,
-                None, lambda: nat.bn_stats(x0s, None, None, None, None, 0.0, 0.0)[0] * float(mr),
-                need_wr)
+                None, lambda: nat.bn_stats_strided(x0, s_r)[0] * float(mr), need_wr)
             if need_wr:
                 dwr = dwrb.view(cout_r, c0, 1, 1)
             dz2d = dzc.permute(0, 2, 3, 1).reshape(mr, cout_r)
-            x02d = x0s.permute(0, 2, 3, 1).reshape(mr, c0)
-            if nat.gemm_dual_supported(cout_r, c0):
-                d0 = torch.empty(mr, c0, dtype=x0.dtype, device=x0.device)
-                nat.gemm_dual_bias(dz2d, x02d, bcat, badd, d0)
+            d0 = torch.empty(mr, c0, dtype=x0.dtype, device=x0.device)
+            if s_r > 1 and nat.gemm_dual_bias_strided(dz2d, x0, s_r, bcat, badd, d0):
+                pass
+            elif nat.gemm_dual_supported(cout_r, c0):
+                nat.gemm_dual_bias(dz2d, x0s().permute(0, 2, 3, 1).reshape(mr, c0), bcat, badd, d0)
             else:
+                x02d = x0s().permute(0, 2, 3, 1).reshape(mr, c0)
                 d0 = torch.addmm(badd.to(x0.dtype), dz2d, bcat[:, :cout_r].t())
                 d0.addmm_(x02d, bcat[:, cout_r:].t())
             d0 = d0.view(nb, ho, wo, c0).permute(0, 3, 1, 2)
