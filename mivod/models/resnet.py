@@ -136,6 +136,9 @@ class Bottleneck(nn.Module):
                                    res_bn=rest[0], res_conv=conv)
                 if conv.stride[0] == 1 and stats_fusable(conv, x):
                     z, part = conv1x1_stats(conv, tap(x), rest[0].running_mean)
+                elif rest[0].training and rest[0].track_running_stats:
+                    # strided shortcut on the 256 x 256 GEMM with its BN's statistics
+                    z, part = downsample_tap(x, conv, rest[0].running_mean)
                 else:
                     z, part = downsample_tap(x, conv), None
                 return conv_bn(self.conv3, self.bn3, out, relu=True, residual=z, res_bn=rest[0],

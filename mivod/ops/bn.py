@@ -173,13 +173,24 @@ class _DownsampleTapConv(torch.autograd.Function):
     (MIOpen strided backward-data: fill + scatter) is ever materialised."""
 
     @staticmethod
-    def forward(ctx, x, w, s, slot):
+    def forward(ctx, x, w, s, slot, shift=None):
         ctx.save_for_backward(x, w)
         ctx.s, ctx.slot = s, slot
-        return F.conv2d(x, w, None, s)
+        # the strided 1x1 conv on the 256 x 256 GEMM (rows gathered at the stride) with the
+        # following BN's statistics in its epilogue, when it covers the shape
+        r = K.native().conv1x1_strided_stats(x, w, s, shift) if _GEMM256 else None
+        if r is None:
+            z, part = F.conv2d(x, w, None, s), torch.empty(0, device=x.device)
+        else:
+            z, part = r[0], (r[1] if shift is not None else torch.empty(0, device=x.device))
+        ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)
+        return z, part
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dpart):
+        if dy is None:
+            return None, None, None, None, None
         x, w = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         dw = None
@@ -192,12 +203,15 @@ class _DownsampleTapConv(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             from .conv import wgrad1x1
             dw = wgrad1x1(dy, x, w, ctx.s)
-        return None, dw, None, None
+        return None, dw, None, None, None
 
 
-def downsample_tap(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+def downsample_tap(x: torch.Tensor, conv: nn.Conv2d, shift=None):
     """``conv(tap(x))`` for a 1x1 strided shortcut conv, fused as _DownsampleTapConv
-    when x's producer reads strided second gradients (fused BN, mode 2)."""
+    when x's producer reads strided second gradients (fused BN, mode 2).  With ``shift``
+    (the following BN's running mean) returns ``(z, partials)``: the conv on the 256 x 256
+    strided GEMM with that BN's statistics in its epilogue, partials None when it does not
+    cover the shape."""
     slot = getattr(x, "_mv_slot", None)
     s = conv.stride[0]
     if (slot is None or not (torch.is_grad_enabled() and x.requires_grad)
@@ -207,8 +221,12 @@ def downsample_tap(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
             or tuple(conv.padding) != (0, 0) or conv.bias is not None or conv.groups != 1
             or x.dtype != torch.bfloat16 or conv.weight.dtype != torch.bfloat16
             or not x.is_contiguous(memory_format=torch.channels_last)):
-        return conv(tap(x))
-    return _DownsampleTapConv.apply(x, conv.weight, s, slot)
+        z = conv(tap(x))
+        return z if shift is None else (z, None)
+    z, part = _DownsampleTapConv.apply(x, conv.weight, s, slot, shift)
+    if shift is None:
+        return z
+    return z, (part if part.numel() else None)
 
 
 def tap(x: torch.Tensor) -> torch.Tensor:

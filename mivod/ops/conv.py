@@ -46,12 +46,25 @@ def _transposed_filter(w: torch.Tensor) -> torch.Tensor:
 
 def dgrad1x1(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """Input gradient of a stride-1 1x1 conv, dX = dY . W as an NHWC GEMM: mivod's
-    256 x 256 kernel (mv_gemm256.hip) when Cin % 256 == 0 and Cout >= 256, else the
-    forward conv with the transposed filter (CK)."""
+    256 x 256 kernel (mv_gemm256.hip) when Cin % 256 == 0 and Cout >= 256, mv_gemm's
+    streaming kernel for Cout in {64, 128, 256} (ResNet-50 layer1.0's 64 -> 64 conv1: CK's
+    forward solver + its output zero fill took 308 + 174 us at bs2048), else the forward
+    conv with the transposed filter (CK)."""
     cout, cin = w.shape[0], w.shape[1]
-    if (os.environ.get("MIVOD_GEMM256", "1") != "0" and cin % 256 == 0 and cout % 64 == 0
-            and cout >= 256 and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and dy.is_contiguous(memory_format=torch.channels_last)):
+    gemm_ok = (dy.is_cuda and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+               and dy.is_contiguous(memory_format=torch.channels_last) and cout % 64 == 0
+               and cin % 64 == 0)
+    if (gemm_ok and os.environ.get("MIVOD_DGRAD1X1_STREAM", "1") != "0" and cin < 256
+            and cout in (64, 128, 256)):
+        from . import kernels as K
+        n, _, h, wd = dy.shape
+        m = n * h * wd
+        dx = torch.empty(m, cin, dtype=dy.dtype, device=dy.device)
+        K.native().gemm_nt(dy.permute(0, 2, 3, 1).reshape(m, cout),
+                           w.reshape(cout, cin).t().contiguous(), dx, None, None)
+        return dx.view(n, h, wd, cin).permute(0, 3, 1, 2)
+    if (gemm_ok and os.environ.get("MIVOD_GEMM256", "1") != "0" and cin % 256 == 0
+            and cout >= 256):
         from . import kernels as K
         n, _, h, wd = dy.shape
         m = n * h * wd

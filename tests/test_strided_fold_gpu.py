@@ -78,3 +78,42 @@ def test_bn_stats_strided_matches_copy(cuda, n, c, h, w, s):
     torch.testing.assert_close(got[0], ref[0], rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(got[0], xs.float().mean((0, 2, 3)), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(got[1], ref[1], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("c,k,h", [(1024, 2048, 14), (256, 512, 9)])
+def test_downsample_tap_stats_matches_conv(cuda, monkeypatch, c, k, h):
+    """The strided shortcut conv on the 256 x 256 GEMM with its BN's statistics partials
+    (ops.bn.downsample_tap(x, conv, shift)) == F.conv2d, partials == sums around shift; the
+    weight gradient and the input gradient (parked in x's producer) match the MIOpen
+    path's."""
+    import copy
+
+    from mivod.ops import bn as B
+    from mivod.ops.conv import Conv2d
+    torch.manual_seed(0)
+    bn0 = B.BatchNorm2d(c).to(cuda)
+    conv = Conv2d(c, k, 1, stride=2, bias=False).to(cuda).to(torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    z0 = _cl(torch.randn(3, c, h, h, device=cuda).to(torch.bfloat16))
+    shift = torch.randn(k, device=cuda) * 0.1
+    grads = []
+    for g256 in (True, False):
+        monkeypatch.setattr(B, "_GEMM256", g256)
+        b0, c2 = copy.deepcopy(bn0), copy.deepcopy(conv)
+        zz = z0.clone().requires_grad_()
+        x = b0(zz, relu=True)
+        z, part = B.downsample_tap(x, c2, shift)
+        ref = torch.nn.functional.conv2d(x.detach().float(), c2.weight.float(), None, 2)
+        torch.testing.assert_close(z.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+        if g256:
+            assert part is not None and torch.isfinite(part).all()
+            d = z.float().permute(0, 2, 3, 1).reshape(-1, k) - shift
+            sm = part.sum(0)
+            torch.testing.assert_close(sm[0], d.sum(0), rtol=1e-3, atol=1e-1)
+            torch.testing.assert_close(sm[1], (d * d).sum(0), rtol=1e-3, atol=1e-1)
+        else:
+            assert part is None
+        z.float().square().mean().backward()
+        grads.append((zz.grad.float(), c2.weight.grad.float()))
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2 * float(b.abs().max()))
