@@ -135,7 +135,10 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   // 2 K-tile buffers + the epilogue's per-channel vectors: ONE LDS object (a second one
   // makes hipcc drain the in-flight LDS DMA before every fragment read)
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * BUF + (NV ? 2 * kVecFloats : 0)];
-  float* vecs = reinterpret_cast<float*>(smem + 2 * BUF);     // [NV][N]
+  // [NV][256]: this workgroup's column tile of the per-channel vectors, then (STATS) the
+  // statistics accumulators [2 wave groups][2][256] summed over all of its output tiles
+  float* vecs = reinterpret_cast<float*>(smem + 2 * BUF);
+  float* stacc = vecs + 4 * BN;
   const int N = p.N;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -145,6 +148,11 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   // share its A rows through that XCD's L2)
   int64_t tile = remap(blockIdx.x, G);
   if (tile >= p.ntiles) return;
+  // G % ntn == 0 (g256_launch): a workgroup's tiles tile, tile + G, ... share one column
+  // tile, so its statistics accumulate on chip and leave as ONE partial row per wave group
+  // (row group tile0 / ntn) — 2 G / ntn partial rows instead of 2 per row block
+  const int64_t tile0 = tile;
+  const int nw0 = (int)(tile0 % p.ntn) * BN;
 
   // ---- staging roles: glds instruction i (0, 1) of a half-tile lands at half row
   // r = (2 w + i) * 8 + lane / 8, LDS chunk lane % 8, which holds source chunk
@@ -371,8 +379,8 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
         f32x4v u = acc[2 * q][b], v = acc[2 * q + 1][b];
         if constexpr (BADD) {
           const int cu = n0 + wn * 64 + 2 * q * 16 + 4 * g;
-          const f32x4v bu = *reinterpret_cast<const f32x4v*>(vecs + cu);
-          const f32x4v bv = *reinterpret_cast<const f32x4v*>(vecs + cu + 16);
+          const f32x4v bu = *reinterpret_cast<const f32x4v*>(vecs + (cu - n0));
+          const f32x4v bv = *reinterpret_cast<const f32x4v*>(vecs + (cu - n0) + 16);
           u += bu;
           v += bv;
         }
@@ -388,7 +396,7 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
             for (int j = 0; j < 8; ++j) {
               const float f = (j & 1) ? __uint_as_float(o[j >> 1] & 0xffff0000u)
                                       : __uint_as_float(o[j >> 1] << 16);
-              const float d = f - vecs[c0 + j];
+              const float d = f - vecs[c0 - n0 + j];
               s1[q][j] += d;
               s2[q][j] += d * d;
             }
@@ -397,9 +405,9 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
         if constexpr (EPI == 4) {
           if (in) {
             const uint32_t xw[4] = {xr[b & 1][q].x, xr[b & 1][q].y, xr[b & 1][q].z, xr[b & 1][q].w};
-            const float* mean = vecs + N;
-            const float* scv = vecs + 2 * N;
-            const float* biv = vecs + 3 * N;
+            const float* mean = vecs + BN - n0;      // indexed by the global column c0 + j
+            const float* scv = vecs + 2 * BN - n0;
+            const float* biv = vecs + 3 * BN - n0;
             float dv[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -430,17 +438,17 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
             s1[q][j] += __shfl_xor(s1[q][j], o, kWave);
             s2[q][j] += __shfl_xor(s2[q][j], o, kWave);
           }
+      // each (wave, lane group) owns its 16 columns of the accumulator: no other wave
+      // touches them, so no barrier (fixed order: the workgroup's tiles in sequence)
       if (rl == 0) {
-        float* pr = p.partial + (mt * 2 + wm) * 2 * N;
+        float* ac = stacc + wm * 2 * BN;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const int c0 = n0 + wn * 64 + q * 32 + (g & 1) * 16 + (g >> 1) * 8;
+          const int cl = wn * 64 + q * 32 + (g & 1) * 16 + (g >> 1) * 8;
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            *reinterpret_cast<f32x4v*>(pr + c0 + 4 * h) =
-                f32x4v{s1[q][4 * h], s1[q][4 * h + 1], s1[q][4 * h + 2], s1[q][4 * h + 3]};
-            *reinterpret_cast<f32x4v*>(pr + N + c0 + 4 * h) =
-                f32x4v{s2[q][4 * h], s2[q][4 * h + 1], s2[q][4 * h + 2], s2[q][4 * h + 3]};
+          for (int j = 0; j < 8; ++j) {
+            ac[cl + j] += s1[q][j];
+            ac[BN + cl + j] += s2[q][j];
           }
         }
       }
@@ -451,17 +459,21 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
       for (int b = 0; b < 8; ++b) acc[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
   };
 
-  // per-channel epilogue vectors -> LDS (EPI 1: shift; 4: badd, mean, sc, bi; 6: badd)
+  // this column tile's per-channel epilogue vectors -> LDS (EPI 1: shift; 4: badd, mean,
+  // sc, bi; 6: badd); zeroed statistics accumulators
   if constexpr (NV > 0) {
-    for (int c = tid; c < N; c += NT) {
-      if constexpr (EPI == 1) vecs[c] = p.shift ? p.shift[c] : 0.f;
-      if constexpr (BADD) vecs[c] = p.badd ? p.badd[c] : 0.f;
+    for (int c = tid; c < BN; c += NT) {
+      const int gc = nw0 + c;
+      if constexpr (EPI == 1) vecs[c] = p.shift ? p.shift[gc] : 0.f;
+      if constexpr (BADD) vecs[c] = p.badd ? p.badd[gc] : 0.f;
       if constexpr (EPI == 4) {
-        vecs[N + c] = p.mean[c];
-        vecs[2 * N + c] = p.sc[c];
-        vecs[3 * N + c] = p.bi[c];
+        vecs[BN + c] = p.mean[gc];
+        vecs[2 * BN + c] = p.sc[gc];
+        vecs[3 * BN + c] = p.bi[gc];
       }
     }
+    if constexpr (STATS)
+      for (int c = tid; c < 4 * BN; c += NT) stacc[c] = 0.f;
   }
   // prologue: this workgroup's first tile, K tile 0, in the consumption order A0, B0,
   // B1, A1; A0 + B0 retired
@@ -551,6 +563,14 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
     }
   }
   if (wm == 0) barrier();          // close the stagger: equal barrier counts
+  if constexpr (STATS) {
+    // partial row (tile0 / ntn) * 2 + wm: this wave's 64 columns of the column tile
+    __syncthreads();
+    float* pr = p.partial + ((tile0 / p.ntn) * 2 + wm) * 2 * N + nw0;
+    const float* ac = stacc + wm * 2 * BN;
+    pr[wn * 64 + lane] = ac[wn * 64 + lane];
+    pr[N + wn * 64 + lane] = ac[BN + wn * 64 + lane];
+  }
 }
 
 // ===========================================================================
@@ -808,10 +828,18 @@ bool mv_gemm256_supported(int64_t M, int N, int K) {
          (int64_t)N * K * 2 < (int64_t(1) << 32);
 }
 
-// two statistics rows (one per M wave group) per row block
+// persistent grid: one workgroup per CU, a multiple of the column-tile count so that every
+// workgroup keeps one column tile (its statistics accumulate on chip)
+static int64_t g256_grid(int64_t M, int N) {
+  const int64_t ntn = N / mv::g256::BN, bm = g256_bm(M, N);
+  const int64_t ntiles = (M + bm - 1) / bm * ntn, cus = g256_cus();
+  const int64_t g = (ntiles < cus ? ntiles : cus) / ntn * ntn;
+  return g > ntn ? g : ntn;
+}
+
+// two statistics rows (one per M wave group) per row group of G / ntn workgroups
 int64_t mv_gemm256_partials(int64_t M, int N) {
-  const int bm = g256_bm(M, N);
-  return 2 * ((M + bm - 1) / bm);
+  return 2 * (g256_grid(M, N) / (N / mv::g256::BN));
 }
 
 template <int EPI, int AMODE>
@@ -820,8 +848,7 @@ static void g256_launch(mv::g256::Args a, hipStream_t st) {
   const int bm = g256_bm(a.M, a.N);
   a.ntn = a.N / BN;
   a.ntiles = (a.M + bm - 1) / bm * a.ntn;
-  const int cus = g256_cus();
-  const dim3 grid((unsigned)(a.ntiles < cus ? a.ntiles : cus));
+  const dim3 grid((unsigned)g256_grid(a.M, a.N));
   if (bm == 224)
     hipLaunchKernelGGL((gemm256_kernel<EPI, AMODE, 7>), grid, dim3(NT), 0, st, a);
   else

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--all", action="store_true")
     ap.add_argument("--title", default="")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--detail", default="",
+                    help="also list every launch (one step) of kernels containing this text, "
+                         "with its duration and the kernel that ran before it")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, stream_id, start, end from kernels order by start").fetchall()
@@ -57,6 +60,17 @@ def main():
         print(f"| {v / steps:.3f} | {100 * v / busy:.1f} | {cnt[n] / steps:.1f} | "
               f"{','.join(map(str, sorted(streams[n])))} | `{nm}` |")
 
+    if a.detail:
+        per = len(win) // max(steps, 1)
+        last = win[-per:]
+        print(f"\n## Launches of `{a.detail}` in the last step\n")
+        print("| us | previous kernel |\n|---:|---|")
+        for i, (n, s_, t0, t1) in enumerate(last):
+            if a.detail in n:
+                prev = last[i - 1][0] if i else "-"
+                prev = prev if len(prev) <= 90 else prev[:87] + "..."
+                print(f"| {(t1 - t0) / 1e3:.1f} | `{prev}` |")
 
 if __name__ == "__main__":
     main()
+
