@@ -1155,10 +1155,10 @@ std::vector<at::Tensor> fold_products(at::Tensor w, at::Tensor g, c10::optional<
 // (7x7 / 2 / pad 3 on a 4-channel 224x224 NHWC image) with BN statistics around shift
 std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> shift,
                                  int64_t grid) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 4 &&
-                  x.size(2) == 224 && x.size(3) == 224 &&
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  (x.size(1) == 4 || x.size(1) == 3) && x.size(2) == 224 && x.size(3) == 224 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "stem_fwd: x must be a channels_last bf16 [N, 4, 224, 224] GPU tensor");
+              "stem_fwd: x must be a channels_last bf16 [N, 3 or 4, 224, 224] GPU tensor");
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == 64 &&
                   w.size(1) == 4 && w.size(2) == 7 && w.size(3) == 7 &&
                   w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.device() == x.device(),
@@ -1181,16 +1181,16 @@ std::vector<at::Tensor> stem_fwd(at::Tensor x, at::Tensor w, c10::optional<at::T
   const int g = grid > 0 ? (int)grid : mv_stem_partials((int)N);
   at::Tensor part = at::empty({(int64_t)g, 2, 64}, x.options().dtype(at::kFloat));
   mv_stem_fwd(x.data_ptr(), w.data_ptr(), z.data_ptr(), sp, part.data_ptr<float>(), (int)N,
-              cur_stream(), g);
+              cur_stream(), g, (int)x.size(1));
   return {z, part};
 }
 
 // dw [64, 4, 7, 7] channels_last bf16: the stem conv's weight gradient (mv_stem.hip)
 at::Tensor stem_wgrad(at::Tensor x, at::Tensor dz) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 4 &&
-                  x.size(2) == 224 && x.size(3) == 224 &&
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  (x.size(1) == 4 || x.size(1) == 3) && x.size(2) == 224 && x.size(3) == 224 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "stem_wgrad: x must be a channels_last bf16 [N, 4, 224, 224] GPU tensor");
+              "stem_wgrad: x must be a channels_last bf16 [N, 3 or 4, 224, 224] GPU tensor");
   const int64_t N = x.size(0);
   TORCH_CHECK(dz.is_cuda() && dz.scalar_type() == at::kBFloat16 && dz.dim() == 4 &&
                   dz.size(0) == N && dz.size(1) == 64 && dz.size(2) == 112 && dz.size(3) == 112 &&
@@ -1202,7 +1202,7 @@ at::Tensor stem_wgrad(at::Tensor x, at::Tensor dz) {
                               x.options().dtype(at::kFloat));
   at::Tensor dw = at::empty({64, 4, 7, 7}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   mv_stem_wgrad(x.data_ptr(), dz.data_ptr(), dw.data_ptr(), work.data_ptr<float>(), (int)N,
-                cur_stream());
+                cur_stream(), (int)x.size(1));
   return dw;
 }
 
@@ -1430,11 +1430,25 @@ int64_t conv3x3_partials(int64_t M, int64_t K) { return mv_conv3x3_partials(M, (
 // y = conv3x3(x, w, stride, pad 1) / conv1x1(x, w, stride) (+ BN statistics partials of y
 // around shift)
 at::Tensor conv_nhwc(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> shift,
-                     c10::optional<at::Tensor> partial, int64_t ks);
+                     c10::optional<at::Tensor> partial, int64_t ks,
+                     c10::optional<at::Tensor> in_scale = c10::nullopt,
+                     c10::optional<at::Tensor> in_bias = c10::nullopt);
 
+// (in_scale, in_bias: x is the producing BN's input; relu(x * in_scale + in_bias) is
+// convolved without being materialised — the 64 -> 64 stride-1 row-patch kernel only)
 at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> shift,
-                   c10::optional<at::Tensor> partial) {
-  return conv_nhwc(x, w, stride, shift, partial, 3);
+                   c10::optional<at::Tensor> partial, c10::optional<at::Tensor> in_scale,
+                   c10::optional<at::Tensor> in_bias) {
+  return conv_nhwc(x, w, stride, shift, partial, 3, in_scale, in_bias);
+}
+
+static const float* opt_vec(const c10::optional<at::Tensor>& t, int64_t n, const at::Tensor& like,
+                            const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                  t->numel() == n && t->device() == like.device(),
+              what, " must be a contiguous fp32 [", n, "] tensor on the input's device");
+  return t->data_ptr<float>();
 }
 
 at::Tensor conv1x1_mfma(at::Tensor x, at::Tensor w, int64_t stride,
@@ -1443,7 +1457,8 @@ at::Tensor conv1x1_mfma(at::Tensor x, at::Tensor w, int64_t stride,
 }
 
 at::Tensor conv_nhwc(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> shift,
-                     c10::optional<at::Tensor> partial, int64_t ks) {
+                     c10::optional<at::Tensor> partial, int64_t ks,
+                     c10::optional<at::Tensor> in_scale, c10::optional<at::Tensor> in_bias) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv3x3: x must be a channels_last bf16 GPU tensor [N, C, H, W]");
@@ -1477,8 +1492,12 @@ at::Tensor conv_nhwc(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<a
       sp = shift->data_ptr<float>();
     }
   }
+  const float* isc = opt_vec(in_scale, C, x, "conv: in_scale");
+  const float* ibi = opt_vec(in_bias, C, x, "conv: in_bias");
+  TORCH_CHECK((isc == nullptr) == (ibi == nullptr), "conv: in_scale and in_bias go together");
   TORCH_CHECK(mv_conv_nhwc(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W,
-                           (int)C, (int)K, (int)ks, (int)stride, sp, pp, cur_stream()),
+                           (int)C, (int)K, (int)ks, (int)stride, sp, pp, cur_stream(), nullptr,
+                           nullptr, isc, ibi),
               "conv: unsupported shape");
   return y;
 }
@@ -1570,7 +1589,8 @@ std::vector<at::Tensor> conv3x3_s2_dgrad(at::Tensor dy, at::Tensor wt, int64_t H
 }
 
 // weight gradient of y = conv3x3(x, w, stride, pad 1): dw [K, C, 3, 3] channels_last bf16
-at::Tensor wgrad3x3(at::Tensor x, at::Tensor dy, int64_t stride) {
+at::Tensor wgrad3x3(at::Tensor x, at::Tensor dy, int64_t stride,
+                    c10::optional<at::Tensor> in_scale, c10::optional<at::Tensor> in_bias) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "wgrad3x3: x must be a channels_last bf16 GPU tensor");
@@ -1588,8 +1608,12 @@ at::Tensor wgrad3x3(at::Tensor x, at::Tensor dy, int64_t stride) {
   at::Tensor work = at::empty({mv_wgrad3x3_workspace(M, (int)K, (int)C)},
                               x.options().dtype(at::kFloat));
   at::Tensor dw = at::empty({K, C, 3, 3}, x.options(), at::MemoryFormat::ChannelsLast);
+  const float* isc = opt_vec(in_scale, C, x, "wgrad3x3: in_scale");
+  const float* ibi = opt_vec(in_bias, C, x, "wgrad3x3: in_bias");
+  TORCH_CHECK((isc == nullptr) == (ibi == nullptr), "wgrad3x3: in_scale and in_bias go together");
   TORCH_CHECK(mv_wgrad3x3(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), work.data_ptr<float>(),
-                          (int)N, (int)H, (int)W, (int)C, (int)K, (int)stride, cur_stream()),
+                          (int)N, (int)H, (int)W, (int)C, (int)K, (int)stride, cur_stream(), isc,
+                          ibi),
               "wgrad3x3: unsupported shape");
   return dw;
 }
@@ -1737,9 +1761,11 @@ PYBIND11_MODULE(_mvk, m) {
         "BN backward finalize only: [5, C] = (dgamma, dbeta, ca, cb, cc) from partials");
   m.def("bn_bwd_from_partials", &bn_bwd_from_partials,
         "BN backward finalize + dx from GEMM-epilogue partials -> (dx, dgamma, dbeta)");
-  m.def("conv3x3", &conv3x3, "implicit-GEMM 3x3 conv (pad 1) with optional fused BN statistics",
+  m.def("conv3x3", &conv3x3, "implicit-GEMM 3x3 conv (pad 1) with optional fused BN statistics "
+        "(in_scale / in_bias: x is the producing BN's input, its BN + ReLU applied on load)",
         py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("shift") = py::none(),
-        py::arg("partial") = py::none());
+        py::arg("partial") = py::none(), py::arg("in_scale") = py::none(),
+        py::arg("in_bias") = py::none());
   m.def("conv1x1", &conv1x1_mfma, "1x1 conv (implicit-GEMM kernel) with optional fused BN statistics",
         py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("shift") = py::none(),
         py::arg("partial") = py::none());
@@ -1754,7 +1780,8 @@ PYBIND11_MODULE(_mvk, m) {
         py::arg("x"), py::arg("dy"), py::arg("stride") = 1, py::arg("fp32_out") = false,
         py::arg("dy2") = py::none());
   m.def("wgrad3x3", &wgrad3x3, "3x3 (pad 1) conv weight gradient on MFMA (transposed LDS reads)",
-        py::arg("x"), py::arg("dy"), py::arg("stride") = 1);
+        py::arg("x"), py::arg("dy"), py::arg("stride") = 1, py::arg("in_scale") = py::none(),
+        py::arg("in_bias") = py::none());
   m.def("conv3x3_partials", &conv3x3_partials, "partial rows of conv3x3's statistics epilogue");
   m.def("gemm_partials", &gemm_partials, "row tiles (statistics partial rows) of gemm_nt");
   m.def("gemm256_nt", &gemm256_nt, "C = A . B^T on the 256x256 glds-pipelined kernel alone");

@@ -17,15 +17,21 @@ bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int 
                 const void* bn_x = nullptr, const float* bn_vec = nullptr);
 
 // same kernel for ks = 1 (pad 0) or 3 (pad 1): y[N, Ho, Wo, K] = conv(x[N, H, W, C], w[K, ks, ks, C])
+// in_scale / in_bias ([C] each, the 64 -> 64 row-patch kernel only — false elsewhere): x is
+// the producing BN's INPUT and relu(x * in_scale + in_bias) is convolved
 bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, int C, int K, int ks,
                   int stride, const float* shift, float* partial, hipStream_t st,
-                  const void* bn_x = nullptr, const float* bn_vec = nullptr);
+                  const void* bn_x = nullptr, const float* bn_vec = nullptr,
+                  const float* in_scale = nullptr, const float* in_bias = nullptr);
 
 // 3x3 weight gradient: dw[K, 3, 3, C] (bf16, channels_last [K, C, 3, 3]) of
 // y = conv3x3(x, w, stride, pad 1) given dy; work: fp32 [mv_wgrad3x3_workspace(M, K, C)]
 int64_t mv_wgrad3x3_workspace(int64_t M, int K, int C);
+// (in_scale / in_bias: as mv_conv_nhwc's — the weight gradient w.r.t. relu(x * in_scale +
+// in_bias); the 64 -> 64 row-patch kernel only)
 bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
-                 int K, int stride, hipStream_t st);
+                 int K, int stride, hipStream_t st, const float* in_scale = nullptr,
+                 const float* in_bias = nullptr);
 
 // 1x1 (pad 0, stride 1/2) weight gradient: dw[K, C] (bf16) of y = conv1x1(x, w, stride)
 // given dy; work: fp32 [mv_wgrad1x1_workspace(M, K, C)], M = N * Ho * Wo
@@ -43,15 +49,18 @@ bool mv_wgrad1x1(const void* x, const void* dy, void* dw, float* work, int N, in
 // workgroups (= the partial-row count when partial != null).  Same epilogues as
 // mv_conv3x3 (statistics / BN+ReLU backward reduce).
 bool mv_conv64_supported(int N, int H, int W, int C, int K, int ks, int stride);
+// in_scale / in_bias (64 each): x is the producing BN's INPUT and relu(x * in_scale +
+// in_bias) is convolved (applied while staging the patch; the BN output never exists)
 bool mv_conv64(const void* x, const void* w, void* y, int N, int H, int W, const float* shift,
                float* partial, int grid, hipStream_t st, const void* bn_x = nullptr,
-               const float* bn_vec = nullptr);
+               const float* bn_vec = nullptr, const float* in_scale = nullptr,
+               const float* in_bias = nullptr);
 // weight gradient of the 64 -> 64 3x3 / stride 1 conv on the row-patch scheme
 // (mv_conv64.hip): W % 4 == 0, W <= 56; writes fp32 partial [grid][9][64][64] rows for
 // mv_conv.hip's wgrad reduce
 bool mv_wgrad64_supported(int N, int H, int W, int C, int K, int stride);
 bool mv_wgrad64(const void* x, const void* dy, float* partial, int grid, int N, int H, int W,
-                hipStream_t st);
+                hipStream_t st, const float* in_scale = nullptr, const float* in_bias = nullptr);
 
 // Stride-2 3x3 (pad 1) data gradient as four output-parity-class gather GEMMs (no zero
 // fill, no structurally-zero products): dy [Nb, H/2, W/2, K], wt = the transposed flipped

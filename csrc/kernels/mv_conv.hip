@@ -441,10 +441,12 @@ bool mv_conv3x3(const void* x, const void* w, void* y, int N, int H, int W, int 
 
 bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, int C, int K, int ks,
                   int stride, const float* shift, float* partial, hipStream_t st,
-                  const void* bn_x, const float* bn_vec) {
+                  const void* bn_x, const float* bn_vec, const float* in_scale,
+                  const float* in_bias) {
   using namespace mv::conv;
   if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2) || (ks != 1 && ks != 3))
     return false;
+  const bool bna = in_scale != nullptr;
   // 64 -> 64 channel 3x3 stride 1 (ResNet-50 layer1): the row-patch kernel (mv_conv64.hip)
   static const bool c64 = [] {
     const char* e = std::getenv("MIVOD_CONV64");
@@ -461,8 +463,10 @@ bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, in
         cus = 256;
       grid = cus;
     }
-    return mv_conv64(x, w, y, N, H, W, shift, partial, grid, st, bn_x, bn_vec);
+    return mv_conv64(x, w, y, N, H, W, shift, partial, grid, st, bn_x, bn_vec, in_scale,
+                     in_bias);
   }
+  if (bna) return false;          // the input BN apply: the row-patch kernel only
   if (conv256_route(K))      // (a shape it cannot take is an error: the partial rows differ)
     return mv_conv256(x, w, y, N, H, W, C, K, ks, stride, shift, partial, bn_x, bn_vec, st);
   Geo g;
@@ -758,9 +762,11 @@ int64_t mv_wgrad3x3_workspace(int64_t M, int K, int C) {
 }
 
 bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, int H, int W, int C,
-                 int K, int stride, hipStream_t st) {
+                 int K, int stride, hipStream_t st, const float* in_scale, const float* in_bias) {
   using namespace mv::conv;
   if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2)) return false;
+  const bool bna = in_scale != nullptr;
+  if (bna && !mv_wgrad64_supported(N, H, W, C, K, stride)) return false;
   Geo g;
   g.H = H;
   g.W = W;
@@ -773,7 +779,7 @@ bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, in
   const int nkc = (K / 64) * (C / 64);
   const int64_t nchunks = (g.M + 31) / 32;
   const int ms = wgrad_msplit(nchunks, nkc);
-  if (w256_3x3_on() && mv_wgrad256_3x3_supported(N, H, W, C, K, stride) &&
+  if (!bna && w256_3x3_on() && mv_wgrad256_3x3_supported(N, H, W, C, K, stride) &&
       mv_wgrad256_3x3(x, dy, work, N, H, W, C, K, stride, st)) {
     const int P = (int)mv_wgrad256_3x3_splits(N, H, W, C, K, stride);
     const int64_t E = (int64_t)9 * K * C;       // [K][9][C] = the channels_last filter
@@ -786,7 +792,7 @@ bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, in
     const char* e = std::getenv("MIVOD_WGRAD64");
     return !(e && e[0] == '0');
   }();
-  if (w64 && mv_wgrad64_supported(N, H, W, C, K, stride)) {
+  if ((w64 || bna) && mv_wgrad64_supported(N, H, W, C, K, stride)) {
     // 64 -> 64 stride 1: the row-patch kernel (mv_conv64.hip), one persistent 136-KB-LDS
     // workgroup per CU (<= ms partial rows, so the workspace above is large enough)
     static const int cus = [] {
@@ -798,7 +804,7 @@ bool mv_wgrad3x3(const void* x, const void* dy, void* dw, float* work, int N, in
       return n;
     }();
     const int grid = ms < cus ? ms : cus;
-    mv_wgrad64(x, dy, work, grid, N, H, W, st);
+    mv_wgrad64(x, dy, work, grid, N, H, W, st, in_scale, in_bias);
     const int64_t n = (int64_t)9 * K * C;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                        (const float*)work, (__bf16*)dw, K, C, grid);

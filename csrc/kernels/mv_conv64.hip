@@ -71,11 +71,28 @@ struct Geo64 {
   int64_t tiles;        // N * hblocks
 };
 
+// The producing BN + ReLU applied while staging (xsc != null): X is that BN's INPUT z and
+// the patch holds bf16(relu(z * xsc + xbi)) — the BN output is never materialised (padding
+// taps stay 0).  Each staging thread owns one fixed 8-channel chunk, so its 16 affine
+// coefficients live in registers.
+__device__ __forceinline__ void bn_relu8(u32x4& v, const float (&sc)[8], const float (&bi)[8]) {
+  uint32_t w[4] = {v[0], v[1], v[2], v[3]};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float lo = fmaxf(__builtin_fmaf(__uint_as_float(w[j] << 16), sc[2 * j], bi[2 * j]), 0.f);
+    const float hi =
+        fmaxf(__builtin_fmaf(__uint_as_float(w[j] & 0xffff0000u), sc[2 * j + 1], bi[2 * j + 1]), 0.f);
+    w[j] = cvt_pk_bf16(lo, hi);
+  }
+  v = u32x4{w[0], w[1], w[2], w[3]};
+}
+
 template <int EPI>
 __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv64_kernel(
     const __bf16* __restrict__ X, const __bf16* __restrict__ Wt, __bf16* __restrict__ Y,
     Geo64 g, const float* __restrict__ shift, float* __restrict__ partial,
-    const __bf16* __restrict__ bnx, const float* __restrict__ bnvec) {
+    const __bf16* __restrict__ bnx, const float* __restrict__ bnvec,
+    const float* __restrict__ xsc, const float* __restrict__ xbi) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[kFilt + kPR * kPW * kC];   // 152 KB
   __bf16* fs = lds;                 // filter
   __bf16* ps = lds + kFilt;         // patch
@@ -113,6 +130,14 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
   const bool colok = scol >= 1 && scol - 1 < W;
   const int64_t coff = (int64_t)(scol - 1) * kC + sch * 8;
   const int soff = pidx(0, scol, sch);              // + row * kPW * 64
+  // (never on the data-gradient variant: its input is a gradient)
+  const bool bna = EPI != 2 && xsc != nullptr;      // (wave-uniform)
+  float asc[8], abi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    asc[j] = bna ? xsc[sch * 8 + j] : 0.f;
+    abi[j] = bna ? xbi[sch * 8 + j] : 0.f;
+  }
   u32x4 pre[kLoads];
   auto gload = [&](int64_t t) {
     const int n = (int)(t / g.hblocks), h0 = (int)(t - (int64_t)n * g.hblocks) * kR;
@@ -259,9 +284,21 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
   // Tile loop: [patch j -> LDS] [epilogue of j-1] [issue loads of j+1] [compute j]: the
   // stores of j-1 and the loads of j+1 fly during j's MFMAs.  The only wait on the memory
   // pipe is for the loads of tile j, issued a whole tile earlier.
+  // the producing BN + ReLU on the in-image pixels of tile tt's prefetched patch rows
+  auto bn_stage = [&](int64_t tt) {
+    const int h0 = (int)(tt - (tt / g.hblocks) * g.hblocks) * kR;
+#pragma unroll
+    for (int i = 0; i < kLoads; ++i) {
+      const int ih = h0 + i - 1;
+      if (colok && ih >= 0 && ih < H) bn_relu8(pre[i], asc, abi);
+    }
+  };
   int64_t t = blockIdx.x;
   int64_t tprev = -1;
-  if (t < g.tiles) gload(t);
+  if (t < g.tiles) {
+    gload(t);
+    if (bna) bn_stage(t);
+  }
   for (; t < g.tiles; t += gridDim.x) {
     __syncthreads();                      // previous tile's patch reads done (and filter stored)
 #pragma unroll
@@ -285,6 +322,13 @@ __global__ __launch_bounds__(kThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 
       frags(st, wA, xA);
       mmas(wA, xA);
       __builtin_amdgcn_sched_barrier(0);
+      // the next tile's BN + ReLU mid-tile: its rows have had half a tile to arrive, and the
+      // VALU work overlaps the other wave's MFMAs on this SIMD (at the barrier both waves
+      // would be doing it at once)
+      if (st == 8 && bna && t + gridDim.x < g.tiles) {
+        bn_stage(t + gridDim.x);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     tprev = t;
   }
@@ -333,7 +377,8 @@ bool mv_conv64_supported(int N, int H, int W, int C, int K, int ks, int stride) 
 
 // grid = `grid` persistent workgroups (the caller's partial-row count)
 bool mv_conv64(const void* x, const void* w, void* y, int N, int H, int W, const float* shift,
-               float* partial, int grid, hipStream_t st, const void* bn_x, const float* bn_vec) {
+               float* partial, int grid, hipStream_t st, const void* bn_x, const float* bn_vec,
+               const float* in_scale, const float* in_bias) {
   using namespace mv::conv64;
   if (!mv_conv64_supported(N, H, W, 64, 64, 3, 1) || grid < 1) return false;
   Geo64 g;
@@ -345,16 +390,17 @@ bool mv_conv64(const void* x, const void* w, void* y, int N, int H, int W, const
   const __bf16* X = (const __bf16*)x;
   const __bf16* Wt = (const __bf16*)w;
   __bf16* Y = (__bf16*)y;
+  if ((in_scale == nullptr) != (in_bias == nullptr) || (bn_x && in_scale)) return false;
   if (bn_x) {
     if (!partial) return false;
     hipLaunchKernelGGL(conv64_kernel<2>, dim3(grid), dim3(kThreads), 0, st, X, Wt, Y, g,
-                       nullptr, partial, (const __bf16*)bn_x, bn_vec);
+                       nullptr, partial, (const __bf16*)bn_x, bn_vec, in_scale, in_bias);
   } else if (partial) {
     hipLaunchKernelGGL(conv64_kernel<1>, dim3(grid), dim3(kThreads), 0, st, X, Wt, Y, g,
-                       shift, partial, nullptr, nullptr);
+                       shift, partial, nullptr, nullptr, in_scale, in_bias);
   } else {
     hipLaunchKernelGGL(conv64_kernel<0>, dim3(grid), dim3(kThreads), 0, st, X, Wt, Y, g,
-                       nullptr, nullptr, nullptr, nullptr);
+                       nullptr, nullptr, nullptr, nullptr, in_scale, in_bias);
   }
   return true;
 }
@@ -405,7 +451,8 @@ __device__ __forceinline__ bf16x8 tr8p(const __bf16* pa, const __bf16* pb) {
 
 __global__ __launch_bounds__(kWThreads, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void wgrad64_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ DY,
-                    float* __restrict__ partial, Geo64 g) {
+                    float* __restrict__ partial, Geo64 g, const float* __restrict__ xsc,
+                    const float* __restrict__ xbi) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[kDyPix * kC + kPR * kPC * kPS];   // 147 KB
   __bf16* ds = lds;
   __bf16* ps = lds + kDyPix * kC;
@@ -421,6 +468,14 @@ void wgrad64_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ DY,
   const int sch = tid & 7, spix = tid >> 3;
   const bool colok = spix >= 1 && spix - 1 < W;
   const int64_t xcoff = (int64_t)(spix - 1) * kC + sch * 8;
+  // X = the producing BN's input z when xsc != null: the patch holds relu(z * xsc + xbi)
+  const bool bna = xsc != nullptr;
+  float asc[8], abi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    asc[j] = bna ? xsc[sch * 8 + j] : 0.f;
+    abi[j] = bna ? xbi[sch * 8 + j] : 0.f;
+  }
   u32x4 pdy[kWLoadsDy], px[kWLoadsX];
   auto gload = [&](int64_t t) {
     const int n = (int)(t / g.hblocks), h0 = (int)(t - (int64_t)n * g.hblocks) * kR;
@@ -465,10 +520,19 @@ void wgrad64_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ DY,
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) acc[u][tp] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
+  auto bn_stage = [&](int64_t tt) {      // the producing BN + ReLU on tile tt's patch rows
+    const int h0 = (int)(tt - (tt / g.hblocks) * g.hblocks) * kR;
+#pragma unroll
+    for (int i = 0; i < kWLoadsX; ++i) {
+      const int ih = h0 + i - 1;
+      if (colok && ih >= 0 && ih < H) bn_relu8(px[i], asc, abi);
+    }
+  };
   int64_t t = blockIdx.x;
   if (t < g.tiles) gload(t);
   for (; t < g.tiles; t += gridDim.x) {
     __syncthreads();                      // previous tile's reads done
+    if (bna) bn_stage(t);                 // (mid-loop placement measured slower here)
     if (spix < kPC) {
 #pragma unroll
       for (int i = 0; i < kWLoadsX; ++i)
@@ -540,7 +604,7 @@ bool mv_wgrad64_supported(int N, int H, int W, int C, int K, int stride) {
 }
 
 bool mv_wgrad64(const void* x, const void* dy, float* partial, int grid, int N, int H, int W,
-                hipStream_t st) {
+                hipStream_t st, const float* in_scale, const float* in_bias) {
   using namespace mv::conv64;
   if (!mv_wgrad64_supported(N, H, W, 64, 64, 1) || grid < 1) return false;
   Geo64 g;
@@ -549,7 +613,8 @@ bool mv_wgrad64(const void* x, const void* dy, float* partial, int grid, int N, 
   g.W = W;
   g.hblocks = (H + kR - 1) / kR;
   g.tiles = (int64_t)N * g.hblocks;
+  if ((in_scale == nullptr) != (in_bias == nullptr)) return false;
   hipLaunchKernelGGL(wgrad64_kernel, dim3(grid), dim3(kWThreads), 0, st, (const __bf16*)x,
-                     (const __bf16*)dy, partial, g);
+                     (const __bf16*)dy, partial, g, in_scale, in_bias);
   return true;
 }

@@ -43,6 +43,15 @@ __device__ __forceinline__ f32x4v mfma(const bf16x8& a, const bf16x8& b, const f
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// one input pixel as the 4-channel LDS image wants it: cin = 4 (zero-padded RGB, one 8-byte
+// load) or cin = 3 (the raw RGB image, three 2-byte loads, channel 3 = 0 — no padded copy
+// of the input is ever written)
+__device__ __forceinline__ u32x2 ld_px(const __bf16* x, int64_t pix, int cin) {
+  if (cin == 4) return *reinterpret_cast<const u32x2*>(x + pix * 4);
+  const uint16_t* p = reinterpret_cast<const uint16_t*>(x) + pix * 3;
+  return u32x2{(uint32_t)p[0] | ((uint32_t)p[1] << 16), (uint32_t)p[2]};
+}
+
 // 2 waves/SIMD: 236 VGPRs with the MFMA accumulators in VGPRs (1.21 vs 1.53 ms at 1 wave).
 // Round 2 saw NaN at this bound: the epilogue's bf16 conversion was inline asm, which
 // the compiler's hazard recognizer cannot see into, so it read the VGPR accumulators 0-6
@@ -53,7 +62,8 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const __bf16* __restri
                                                        const __bf16* __restrict__ w,
                                                        __bf16* __restrict__ z,
                                                        const float* __restrict__ shift,
-                                                       float* __restrict__ partial, int N) {
+                                                       float* __restrict__ partial, int N,
+                                                       int cin) {
   __shared__ __attribute__((aligned(16))) __bf16 ws[kCO * kChunks * 8];   // 32 KB
   __shared__ __attribute__((aligned(16))) __bf16 ps[kPatch * kC];         // 14.5 KB
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -89,7 +99,7 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const __bf16* __restri
       const int ih = 2 * oh + r - 3, iw = pc - 3;
       u32x2 v = {0u, 0u};
       if (q < kIR * 230 && ih >= 0 && ih < kH && iw >= 0 && iw < kW)
-        v = *reinterpret_cast<const u32x2*>(x + (((int64_t)n * kH + ih) * kW + iw) * kC);
+        v = ld_px(x, ((int64_t)n * kH + ih) * kW + iw, cin);
       pre[i] = v;
     }
   };
@@ -198,10 +208,10 @@ int mv_stem_partials(int N) {
 }
 
 void mv_stem_fwd(const void* x, const void* w, void* z, const float* shift, float* partial, int N,
-                 hipStream_t st, int grid) {
+                 hipStream_t st, int grid, int cin) {
   if (grid <= 0) grid = mv_stem_partials(N);
   hipLaunchKernelGGL(mv::stem::stem_fwd_kernel, dim3(grid), dim3(256), 0, st, (const __bf16*)x,
-                     (const __bf16*)w, (__bf16*)z, shift, partial, N);
+                     (const __bf16*)w, (__bf16*)z, shift, partial, N, cin);
 }
 
 // ---------------------------------------------------------------- weight gradient
@@ -246,7 +256,8 @@ constexpr int kWLoads = (7 * 230 + 255) / 256;   // 8-byte patch loads per threa
 
 __global__ __launch_bounds__(256) void stem_wgrad_kernel(const __bf16* __restrict__ x,
                                                          const __bf16* __restrict__ dz,
-                                                         float* __restrict__ partial, int N) {
+                                                         float* __restrict__ partial, int N,
+                                                         int cin) {
   __shared__ __attribute__((aligned(16))) __bf16 ps[7 * kPW * kC];        // 13 KB
   __shared__ __attribute__((aligned(16))) __bf16 ds[128 * 64];            // 16 KB
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -273,7 +284,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const __bf16* __restric
       const int ih = 2 * oh + r - 3, iw = pc - 3;
       u32x2 v = {0u, 0u};
       if (q < 7 * 230 && ih >= 0 && ih < kH && iw >= 0 && iw < kW)
-        v = *reinterpret_cast<const u32x2*>(x + (((int64_t)n * kH + ih) * kW + iw) * kC);
+        v = ld_px(x, ((int64_t)n * kH + ih) * kW + iw, cin);
       pp[i] = v;
     }
     const __bf16* dzr = dz + row * (int64_t)kOW * kCO;
@@ -360,10 +371,11 @@ int mv_stem_wgrad_blocks(int N) {
   return (int)g;
 }
 
-void mv_stem_wgrad(const void* x, const void* dz, void* dw, float* work, int N, hipStream_t st) {
+void mv_stem_wgrad(const void* x, const void* dz, void* dw, float* work, int N, hipStream_t st,
+                   int cin) {
   const int G = mv_stem_wgrad_blocks(N);
   hipLaunchKernelGGL(mv::stem::stem_wgrad_kernel, dim3(G), dim3(256), 0, st, (const __bf16*)x,
-                     (const __bf16*)dz, work, N);
+                     (const __bf16*)dz, work, N, cin);
   hipLaunchKernelGGL(mv::stem::stem_wgrad_reduce_kernel, dim3((64 * 196 + 255) / 256), dim3(256), 0,
                      st, work, G, (__bf16*)dw);
 }

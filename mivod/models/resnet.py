@@ -17,8 +17,9 @@ import os
 import torch.nn.functional as F
 
 from ..ops.conv import Conv2d, conv1x1_stats, stats_fusable
-from ..ops.bn import (BatchNorm2d, bn_relu_maxpool, conv_bn, downsample_tap, global_avg_pool,
-                      pad_channels, shortcut_foldable, shortcut_fusable, tap)
+from ..ops import bn as _bn
+from ..ops.bn import (BatchNorm2d, bn_relu_conv3x3, bn_relu_maxpool, conv_bn, downsample_tap,
+                      global_avg_pool, pad_channels, shortcut_foldable, shortcut_fusable, tap)
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -38,6 +39,8 @@ class _StemConvStats(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x4, w4, shift):
+        # x4: the 3-channel image itself (the kernels read RGB pixels and stage them as 4
+        # channels) or a zero-padded 4-channel one
         from ..ops import kernels as K
         z, part = K.native().stem_fwd(x4, w4, shift)
         ctx.save_for_backward(x4, w4)
@@ -56,8 +59,8 @@ class _StemConvStats(torch.autograd.Function):
                 from ..ops import kernels as K
                 dw = K.native().stem_wgrad(x4, dz)
             else:
-                dw = torch.ops.aten.convolution_backward(dz, x4, w4, None, [2, 2], [3, 3], [1, 1],
-                                                         False, [0, 0], 1,
+                dw = torch.ops.aten.convolution_backward(dz, pad_channels(x4, 4), w4, None, [2, 2],
+                                                         [3, 3], [1, 1], False, [0, 0], 1,
                                                          [False, True, False])[1]
         return None, dw, None
 
@@ -82,7 +85,9 @@ class StemConv(nn.Conv2d):
                 or self.bias is not None or self.groups != 1 or tuple(self.dilation) != (1, 1)):
             return None
         w = F.pad(self.weight, (0, 0, 0, 0, 0, 1)).contiguous(memory_format=torch.channels_last)
-        return _StemConvStats.apply(pad_channels(x, 4), w, shift)
+        # the kernels read the 3-channel image directly (MIVOD_STEM_PAD_INPUT=1: pad it first)
+        xin = pad_channels(x, 4) if os.environ.get("MIVOD_STEM_PAD_INPUT", "0") == "1" else x
+        return _StemConvStats.apply(xin, w, shift)
 
     def forward(self, x):
         cp = int(os.environ.get("MIVOD_STEM_CHANNELS", "4"))
@@ -112,10 +117,15 @@ class Bottleneck(nn.Module):
         # conv_bn: a qualifying 1x1 conv computes its BN's statistics in the GEMM
         # epilogue (mivod.ops.conv), so the BN skips its statistics pass; conv1's data
         # gradient also runs the backward reduce of the BN that produced x
-        out = conv_bn(self.conv1, self.bn1, x, relu=True)
-        # 3x3: mivod's implicit-GEMM conv with the BN statistics in its epilogue
-        # (+ column sums of the BN2 output for conv3's folded weight gradient)
-        out = conv_bn(self.conv2, self.bn2, out, relu=True, colsum=True)
+        r = bn_relu_conv3x3(self.conv1, self.bn1, self.conv2, self.bn2, x)
+        if r is not None:
+            # layer1: BN1 + ReLU applied inside conv2's row-patch kernels (never written)
+            out = self.bn2(r[0], relu=True, stats=r[1], colsum=_bn._COLSUM)
+        else:
+            out = conv_bn(self.conv1, self.bn1, x, relu=True)
+            # 3x3: mivod's implicit-GEMM conv with the BN statistics in its epilogue
+            # (+ column sums of the BN2 output for conv3's folded weight gradient)
+            out = conv_bn(self.conv2, self.bn2, out, relu=True, colsum=True)
         # the shortcut's gradient is added inside the backward of the op that
         # produced x (mivod.ops.bn.tap), not by a separate autograd add; a strided
         # 1x1 shortcut conv hands it over at its output resolution (downsample_tap).

@@ -770,6 +770,80 @@ class _Conv1x1BNFold(torch.autograd.Function):
                 dbr if ctx.needs_input_grad[12] else None, None, dwr)
 
 
+class _BNReluConv64(torch.autograd.Function):
+    """``conv3x3(relu(bn1(z1)))`` for the 64 -> 64 stride-1 conv2 of a ResNet-50 layer1
+    bottleneck with BN1 + ReLU applied while the row-patch kernels stage their input patch
+    (csrc/kernels/mv_conv64.hip): the BN1 output is never written (its apply pass was ~0.28
+    ms per block at bs2048) — forward (+ BN2 statistics) and the weight gradient read z1
+    and recompute relu(bn1(z1)) on the fly; the data gradient carries BN1's backward reduce
+    as before (mask from z1 through BN1's affine).  BN1's statistics come from conv1's GEMM
+    epilogue (``part1``); its running statistics update in the finalize.
+    ``MIVOD_BN_APPLY_FUSE=0`` keeps the materialised path (A/B)."""
+
+    @staticmethod
+    def forward(ctx, z1, part1, g1, b1, rm1, rv1, mom1, eps1, w2, shift2):
+        nat = K.native()
+        n, _, h, wd = z1.shape
+        m = n * h * wd
+        vec1 = nat.bn_finalize(part1, g1, b1, rm1, rv1, mom1, eps1, m)
+        k = w2.shape[0]
+        part2 = torch.empty(nat.conv3x3_partials(m, k), 2, k, dtype=torch.float32,
+                            device=z1.device)
+        z2 = nat.conv3x3(z1, w2.contiguous(memory_format=torch.channels_last), 1, shift2, part2,
+                         vec1[2], vec1[3])
+        ctx.save_for_backward(z1, vec1, g1, w2)
+        ctx.mark_non_differentiable(part2)
+        ctx.set_materialize_grads(False)
+        return z2, part2
+
+    @staticmethod
+    def backward(ctx, dz2, _dpart):
+        if dz2 is None:
+            return (None,) * 10
+        from .conv import _transposed_filter
+        z1, vec1, g1, w2 = ctx.saved_tensors
+        nat = K.native()
+        dz2 = _cl(dz2)
+        # conv2's data gradient with BN1's ReLU mask and backward reduce in its epilogue
+        d1, p1 = nat.conv3x3_bn_bwd(dz2, _transposed_filter(w2), z1, vec1)
+        dw2 = (nat.wgrad3x3(z1, dz2, 1, vec1[2], vec1[3]) if ctx.needs_input_grad[8] else None)
+        need_aff = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        dz1, dg1, db1 = nat.bn_bwd_from_partials(d1, z1, vec1, g1, need_aff, p1)
+        return (dz1 if ctx.needs_input_grad[0] else None, None,
+                dg1 if ctx.needs_input_grad[2] else None,
+                db1 if ctx.needs_input_grad[3] else None, None, None, None, None, dw2, None)
+
+
+def bn_relu_conv3x3(conv1: nn.Conv2d, bn1: "BatchNorm2d", conv2: nn.Conv2d, bn2: "BatchNorm2d",
+                    x: torch.Tensor):
+    """``(z2, BN2 statistics partials)`` of ``conv2(relu(bn1(conv1(x))))`` through
+    _BNReluConv64 when it applies (training, 64 -> 64 stride-1 3x3 conv2 on the row-patch
+    kernels, conv1 a statistics-fusable 1x1), else None."""
+    from .conv import bwd_fusable, conv1x1_bn, stats_fusable
+    if (os.environ.get("MIVOD_BN_APPLY_FUSE", "1") == "0" or not torch.is_grad_enabled()
+            or not (bn1.training and bn1.track_running_stats and bn2.training
+                    and bn2.track_running_stats)
+            or bn1.running_mean is None or bn2.running_mean is None or bn1.weight is None
+            or bn1.bias is None or not _fusable(x, bn1.weight)
+            or conv1.out_channels != 64 or conv2.in_channels != 64 or conv2.out_channels != 64
+            or tuple(conv2.kernel_size) != (3, 3) or tuple(conv2.stride) != (1, 1)
+            or tuple(conv2.padding) != (1, 1) or tuple(conv2.dilation) != (1, 1)
+            or conv2.groups != 1 or conv2.bias is not None
+            or conv2.weight.dtype != torch.bfloat16 or not stats_fusable(conv1, x)):
+        return None
+    n, _, h, w = x.shape
+    st = conv1.stride[0]
+    h, w = (h - 1) // st + 1, (w - 1) // st + 1
+    # the row-patch kernels: forward W <= 62 (8 rows x W <= 448 pixels), weight gradient
+    # W % 4 == 0 and W <= 56
+    if not (w <= 56 and w % 4 == 0 and h >= 1):
+        return None
+    z1, part1 = conv1x1_bn(conv1, x, bn1.running_mean, True, bwd_fusable(conv1, x))
+    return _BNReluConv64.apply(z1, part1, bn1.weight, bn1.bias, bn1.running_mean,
+                               bn1.running_var, float(bn1._train_momentum()), float(bn1.eps),
+                               conv2.weight, bn2.running_mean)
+
+
 def _fold_eligible(conv: nn.Conv2d, bn: "BatchNorm2d", x: torch.Tensor, relu, residual) -> bool:
     from .conv import _eligible
     return (os.environ.get("MIVOD_BN_FOLD", "1") != "0" and relu and residual is not None

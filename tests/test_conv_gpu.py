@@ -391,3 +391,20 @@ def test_wgrad64_matches_general_kernel(cuda, n, h, w):
     assert torch.isfinite(dw.float()).all()
     torch.testing.assert_close(dw.float(), ref.float(), rtol=1e-2,
                                atol=1e-2 * float(ref.float().abs().max()))
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_stem_kernels_read_rgb_directly(cuda, n):
+    """The stem kernels on the raw 3-channel image == on its zero-padded 4-channel copy, bit
+    for bit (forward output, statistics partials, weight gradient): no padded input copy."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(50 + n)
+    x3 = _cl(torch.rand(n, 3, 224, 224, device=cuda, generator=g).to(torch.bfloat16))
+    x4 = _cl(F.pad(x3, (0, 0, 0, 0, 0, 1)))
+    w = _cl((torch.randn(64, 4, 7, 7, device=cuda, generator=g) * 0.05).to(torch.bfloat16))
+    shift = torch.randn(64, device=cuda, generator=g) * 0.1
+    z3, p3 = nat.stem_fwd(x3, w, shift, 0)
+    z4, p4 = nat.stem_fwd(x4, w, shift, 0)
+    assert torch.equal(z3, z4) and torch.equal(p3, p4)
+    dz = _cl(torch.randn(n, 64, 112, 112, device=cuda, generator=g).to(torch.bfloat16))
+    assert torch.equal(nat.stem_wgrad(x3, dz), nat.stem_wgrad(x4, dz))
