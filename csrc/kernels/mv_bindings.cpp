@@ -1129,8 +1129,8 @@ std::vector<at::Tensor> fold_products(at::Tensor w, at::Tensor g, c10::optional<
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2,
               "fold_products: W must be contiguous bf16 [cout, cin]");
   const int64_t cout = w.size(0), cin = w.size(1);
-  TORCH_CHECK(cout % 16 == 0 && cin % 16 == 0 && cout > 0 && cin > 0,
-              "fold_products: channels must be positive multiples of 16 (16x16 tiles)");
+  TORCH_CHECK(cout % 64 == 0 && cin % 64 == 0 && cout > 0 && cin > 0,
+              "fold_products: channels must be positive multiples of 64 (64x64 tiles)");
   const auto d = w.device();
   fold_check_f32(g, cout * cin, d, "g");
   fold_check_f32(co, 5 * cout, d, "co");
@@ -1539,13 +1539,11 @@ std::vector<at::Tensor> conv3x3_bn_bwd(at::Tensor dy, at::Tensor wt, at::Tensor 
   return {d, part};
 }
 
-// data gradient of a stride-2 3x3 conv (pad 1) on mv_gemm256's parity-class gather GEMM:
-// dy [N, K, H/2, W/2], wt the transposed flipped filter [C, K, 3, 3] -> dx [N, C, H, W]; with
-// (x_bn, vec): d = relu'(bn(x_bn)) * dx and the producing BN's reduce partials [P, 2, C].
-// Returns [] when the shape is not covered (the caller falls back).
-std::vector<at::Tensor> conv3x3_s2_dgrad(at::Tensor dy, at::Tensor wt, int64_t H, int64_t W,
-                                         c10::optional<at::Tensor> x_bn,
-                                         c10::optional<at::Tensor> vec) {
+// data gradient of a stride-2 3x3 conv (pad 1) as four output-parity-class gather GEMMs
+// (mv_conv.hip / mv_gemm256.hip): dy [N, K, H/2, W/2], wt the transposed flipped filter
+// [C, K, 3, 3] -> dx [N, C, H, W].  Returns [] when the shape is not covered (the caller
+// falls back).
+std::vector<at::Tensor> conv3x3_s2_dgrad(at::Tensor dy, at::Tensor wt, int64_t H, int64_t W) {
   TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
                   dy.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv3x3_s2_dgrad: dy must be a channels_last bf16 GPU tensor");
@@ -1556,35 +1554,14 @@ std::vector<at::Tensor> conv3x3_s2_dgrad(at::Tensor dy, at::Tensor wt, int64_t H
   const int64_t N = dy.size(0), K = dy.size(1), C = wt.size(0);
   TORCH_CHECK(H > 0 && W > 0 && (H - 1) / 2 + 1 == dy.size(2) && (W - 1) / 2 + 1 == dy.size(3),
               "conv3x3_s2_dgrad: H, W do not match dy");
-  const bool bn = x_bn.has_value() && x_bn->defined();
-  // the BN-reduce epilogue only on the 256 x 256 pipeline (dx channels % 256 == 0)
   if (H >= 65536 || W >= 65536 || N >= (int64_t(1) << 31) ||
-      !(bn ? mv_dgrad256_s2_supported((int)N, (int)H, (int)W, (int)C, (int)K)
-           : mv_conv3x3_s2_dgrad_supported((int)N, (int)H, (int)W, (int)C, (int)K)))
+      !mv_conv3x3_s2_dgrad_supported((int)N, (int)H, (int)W, (int)C, (int)K))
     return {};
-  if (bn) {
-    TORCH_CHECK(x_bn->is_cuda() && x_bn->scalar_type() == at::kBFloat16 &&
-                    x_bn->sizes() == at::IntArrayRef({N, C, H, W}) &&
-                    x_bn->is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                    x_bn->device() == dy.device(),
-                "conv3x3_s2_dgrad: x_bn must be the BN input [N, C, H, W], channels_last bf16");
-    TORCH_CHECK(vec.has_value() && vec->is_cuda() && vec->scalar_type() == at::kFloat &&
-                    vec->is_contiguous() && vec->numel() == 4 * C && vec->device() == dy.device(),
-                "conv3x3_s2_dgrad: saved stats must be fp32 [4, C]");
-  }
   c10::DeviceGuard guard(dy.device());
   at::Tensor dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
-  at::Tensor part;
-  if (bn)
-    part = at::empty({mv_dgrad256_s2_partials((int)N, (int)H, (int)W, (int)C), 2, C},
-                     dy.options().dtype(at::kFloat));
-  const bool ok = bn ? mv_dgrad256_s2(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)N, (int)H,
-                                      (int)W, (int)C, (int)K, part.data_ptr<float>(),
-                                      x_bn->data_ptr(), vec->data_ptr<float>(), cur_stream())
-                     : mv_conv3x3_s2_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)N,
-                                           (int)H, (int)W, (int)C, (int)K, cur_stream());
-  TORCH_CHECK(ok, "conv3x3_s2_dgrad: launch refused");
-  if (bn) return {dx, part};
+  TORCH_CHECK(mv_conv3x3_s2_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)N, (int)H,
+                                  (int)W, (int)C, (int)K, cur_stream()),
+              "conv3x3_s2_dgrad: launch refused");
   return {dx};
 }
 
@@ -1772,10 +1749,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("conv3x3_bn_bwd", &conv3x3_bn_bwd,
         "stride-1 3x3 data gradient with the producing BN+ReLU's backward reduce fused");
   m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad,
-        "stride-2 3x3 data gradient (parity-class gather GEMMs), optionally with the producing "
-        "BN+ReLU's backward reduce; [] when the shape is not covered",
-        py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"), py::arg("x_bn") = py::none(),
-        py::arg("vec") = py::none());
+        "stride-2 3x3 data gradient (parity-class gather GEMMs); [] when the shape is not "
+        "covered", py::arg("dy"), py::arg("wt"), py::arg("H"), py::arg("W"));
   m.def("wgrad1x1", &wgrad1x1, "1x1 (pad 0, stride 1/2) conv weight gradient on MFMA",
         py::arg("x"), py::arg("dy"), py::arg("stride") = 1, py::arg("fp32_out") = false,
         py::arg("dy2") = py::none());

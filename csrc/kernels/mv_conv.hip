@@ -522,7 +522,7 @@ bool mv_conv3x3_s2_dgrad(const void* dy, const void* wt, void* dx, int Nb, int H
                          int K, hipStream_t st) {
   using namespace mv::conv;
   if (mv_dgrad256_s2_supported(Nb, H, W, C, K))
-    return mv_dgrad256_s2(dy, wt, dx, Nb, H, W, C, K, nullptr, nullptr, nullptr, st);
+    return mv_dgrad256_s2(dy, wt, dx, Nb, H, W, C, K, st);
   if (!mv_conv3x3_s2_dgrad_supported(Nb, H, W, C, K)) return false;
   Geo g;
   g.ks = 3;

@@ -77,71 +77,119 @@ __global__ __launch_bounds__(kThreads) void fold_coeffs_kernel(
   co[4 * cout + c] = -a * sdz * inv_m - bb * mean;
 }
 
-// 16x16 output tiles (one per workgroup, one element per lane) for the two small GEMMs,
-// staged through LDS in 16-deep chunks; then elementwise jobs.  Block ranges:
-//   [0, n1)            dW tiles   (cout/16 x cin/16):  (W gram)[c][k]
-//   [n1, n1 + n2)      Q tiles    (cin/16 x cin/16):   sum_c W[c][k] cb[c] W[c][j]
-//   [n1 + n2, grid)    bcat[:, :cout] and badd, grid-stride
-constexpr int kT = 16;
+// The two small GEMMs as 64 x 64 output tiles per workgroup, 4 x 4 outputs per lane
+// (register-tiled fp32 FMA, operands staged through LDS 16 deep), then the GEMV and the
+// elementwise jobs.  Block ranges:
+//   [0, n1)                 dW tiles (cout/64 x cin/64):  (W gram)[c][k]
+//   [n1, n1 + n2)           Q tiles  (cin/64 x cin/64):   sum_c W[c][k] cb[c] W[c][j]
+//   [n1 + n2, n1 + n2 + n4) badd, 64 k per block (the 4 waves split c, fixed-order sum)
+//   [n1 + n2 + n4, grid)    bcat[:, :cout], grid-stride
+// (The first version staged 16 x 16 tiles with one output per lane and ran the GEMV as one
+// serial loop per k: ~67 us per launch, 1.0 ms/step at ResNet-50 bs2048.)
+constexpr int kBT = 64, kKC = 16;
 
 __global__ __launch_bounds__(kThreads) void fold_products_kernel(
     const __bf16* __restrict__ w, const float* __restrict__ g, const float* __restrict__ gram,
     const float* __restrict__ co, const float* __restrict__ xsum, int cout, int cin,
     __bf16* __restrict__ dw, __bf16* __restrict__ bcat, float* __restrict__ badd, int n1,
-    int n2) {
+    int n2, int n4) {
   const float* ca = co + 2 * cout;
   const float* cb = co + 3 * cout;
   const float* cc = co + 4 * cout;
   const int ldb = cout + cin;
-  const int ty = threadIdx.x / kT, tx = threadIdx.x % kT;
-  __shared__ float ta[kT][kT + 1], tb[kT][kT + 1];
+  const int tid = threadIdx.x;
   const int b = blockIdx.x;
-  if (b < n1) {                                       // dW tile
-    const int tiles_k = cin / kT;
-    const int c0 = (b / tiles_k) * kT, k0 = (b % tiles_k) * kT;
-    float s = 0.f;
-    for (int j0 = 0; j0 < cin; j0 += kT) {
-      ta[ty][tx] = (float)w[(int64_t)(c0 + ty) * cin + j0 + tx];
-      tb[ty][tx] = gram[(int64_t)(j0 + ty) * cin + k0 + tx];
+  if (b < n1 + n2) {
+    // sa[kk][r] = A[r][k0 + kk], sb[kk][col] = B[k0 + kk][col] (A row-tile, B column-tile)
+    __shared__ __attribute__((aligned(16))) float sa[kKC][kBT + 4], sb[kKC][kBT + 4];
+    const bool is_dw = b < n1;
+    const int t = is_dw ? b : b - n1;
+    const int tiles_n = cin / kBT;
+    const int r0 = (t / tiles_n) * kBT, n0 = (t % tiles_n) * kBT;
+    const int K = is_dw ? cin : cout;
+    const int ty = tid >> 4, tx = tid & 15;          // outputs rows 4 ty.., cols 4 tx..
+    // staging: 4 elements of each tile per lane
+    const int lr = tid >> 2, lk = (tid & 3) * 4;     // A: row lr, k lk..lk+3 / B: k, col
+    float acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = 0.f;
+    for (int k0 = 0; k0 < K; k0 += kKC) {
+      if (is_dw) {
+        // A = W [cout][cin] (row c, k contiguous); B = gram [cin][cin]
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          sa[lk + q][lr] = (float)w[(int64_t)(r0 + lr) * cin + k0 + lk + q];
+        const int bk = tid >> 4, bc = (tid & 15) * 4;
+        const float4 v = *reinterpret_cast<const float4*>(gram + (int64_t)(k0 + bk) * cin + n0 + bc);
+        sb[bk][bc] = v.x;
+        sb[bk][bc + 1] = v.y;
+        sb[bk][bc + 2] = v.z;
+        sb[bk][bc + 3] = v.w;
+      } else {
+        // A[k][c] = W[c][k] cb[c] (row k = r0.., c = k0..); B[c][j] = W[c][j]
+        const int ck = tid >> 4, cr = (tid & 15) * 4;
+        const int c = k0 + ck;
+        const float cbc = cb[c];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sa[ck][cr + q] = (float)w[(int64_t)c * cin + r0 + cr + q] * cbc;
+          sb[ck][cr + q] = (float)w[(int64_t)c * cin + n0 + cr + q];
+        }
+      }
       __syncthreads();
 #pragma unroll
-      for (int jj = 0; jj < kT; ++jj) s += ta[ty][jj] * tb[jj][tx];
-      __syncthreads();
-    }
-    const int c = c0 + ty, k = k0 + tx;
-    const int64_t i = (int64_t)c * cin + k;
-    dw[i] = (__bf16)(ca[c] * g[i] + cb[c] * s + cc[c] * xsum[k]);
-    return;
-  }
-  if (b < n1 + n2) {                                  // Q tile -> bcat[k][cout + j]
-    const int tiles_j = cin / kT, t = b - n1;
-    const int k0 = (t / tiles_j) * kT, j0 = (t % tiles_j) * kT;
-    float s = 0.f;
-    for (int c0 = 0; c0 < cout; c0 += kT) {
-      const int c = c0 + ty;
-      ta[ty][tx] = (float)w[(int64_t)c * cin + k0 + tx] * cb[c];
-      tb[ty][tx] = (float)w[(int64_t)c * cin + j0 + tx];
-      __syncthreads();
+      for (int kk = 0; kk < kKC; ++kk) {
+        const float4 a = *reinterpret_cast<const float4*>(&sa[kk][4 * ty]);
+        const float4 bv = *reinterpret_cast<const float4*>(&sb[kk][4 * tx]);
+        const float av[4] = {a.x, a.y, a.z, a.w}, bw[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
-      for (int q = 0; q < kT; ++q) s += ta[q][ty] * tb[q][tx];
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc[i][jj] = __builtin_fmaf(av[i], bw[jj], acc[i][jj]);
+      }
       __syncthreads();
     }
-    bcat[(int64_t)(k0 + ty) * ldb + cout + j0 + tx] = (__bf16)s;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + 4 * ty + i;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int n = n0 + 4 * tx + jj;
+        if (is_dw) {
+          const int64_t e = (int64_t)r * cin + n;
+          dw[e] = (__bf16)(ca[r] * g[e] + cb[r] * acc[i][jj] + cc[r] * xsum[n]);
+        } else {
+          bcat[(int64_t)r * ldb + cout + n] = (__bf16)acc[i][jj];
+        }
+      }
+    }
     return;
   }
-  const int64_t n_bl = (int64_t)cin * cout, total = n_bl + cin;
-  const int nb3 = gridDim.x - n1 - n2;
-  for (int64_t i = (int64_t)(b - n1 - n2) * kThreads + threadIdx.x; i < total;
+  if (b < n1 + n2 + n4) {                            // badd[k] = sum_c cc[c] W[c][k]
+    __shared__ float red[4][kBT];
+    const int k = (b - n1 - n2) * kBT + (tid & 63), wv = tid >> 6;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int c = wv;
+    for (; c + 12 < cout; c += 16) {
+      s0 += cc[c] * (float)w[(int64_t)c * cin + k];
+      s1 += cc[c + 4] * (float)w[(int64_t)(c + 4) * cin + k];
+      s2 += cc[c + 8] * (float)w[(int64_t)(c + 8) * cin + k];
+      s3 += cc[c + 12] * (float)w[(int64_t)(c + 12) * cin + k];
+    }
+    for (; c < cout; c += 4) s0 += cc[c] * (float)w[(int64_t)c * cin + k];
+    red[wv][tid & 63] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (wv == 0) badd[k] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    return;
+  }
+  const int64_t n_bl = (int64_t)cin * cout;
+  const int nb3 = gridDim.x - n1 - n2 - n4;
+  for (int64_t i = (int64_t)(b - n1 - n2 - n4) * kThreads + tid; i < n_bl;
        i += (int64_t)nb3 * kThreads) {
-    if (i < n_bl) {                                   // bcat[k][c], c fastest
-      const int k = (int)(i / cout), c = (int)(i % cout);
-      bcat[(int64_t)k * ldb + c] = (__bf16)(ca[c] * (float)w[(int64_t)c * cin + k]);
-    } else {                                          // badd[k]
-      const int k = (int)(i - n_bl);
-      float s = 0.f;
-      for (int c = 0; c < cout; ++c) s += cc[c] * (float)w[(int64_t)c * cin + k];
-      badd[k] = s;
-    }
+    const int k = (int)(i / cout), c = (int)(i % cout);     // bcat[k][c], c fastest
+    bcat[(int64_t)k * ldb + c] = (__bf16)(ca[c] * (float)w[(int64_t)c * cin + k]);
   }
 }
 
@@ -159,13 +207,14 @@ void mv_fold_coeffs(const float* part, int P, const void* w, const float* g, con
 void mv_fold_products(const void* w, const float* g, const float* gram, const float* co,
                       const float* xsum, int cout, int cin, void* dw, void* bcat, float* badd,
                       hipStream_t st) {
-  using mv::fold::kT;
-  const int n1 = dw ? (cout / kT) * (cin / kT) : 0;
-  const int n2 = (cin / kT) * (cin / kT);
-  const int64_t rest = (int64_t)cin * cout + cin;
+  using mv::fold::kBT;
+  const int n1 = dw ? (cout / kBT) * (cin / kBT) : 0;
+  const int n2 = (cin / kBT) * (cin / kBT);
+  const int n4 = cin / kBT;
+  const int64_t rest = (int64_t)cin * cout;
   int n3 = (int)((rest + mv::fold::kThreads - 1) / mv::fold::kThreads);
   if (n3 > 1024) n3 = 1024;
-  hipLaunchKernelGGL(mv::fold::fold_products_kernel, dim3((unsigned)(n1 + n2 + n3)),
+  hipLaunchKernelGGL(mv::fold::fold_products_kernel, dim3((unsigned)(n1 + n2 + n4 + n3)),
                      dim3(mv::fold::kThreads), 0, st, (const __bf16*)w, g, gram, co, xsum, cout,
-                     cin, (__bf16*)dw, (__bf16*)bcat, badd, n1, n2);
+                     cin, (__bf16*)dw, (__bf16*)bcat, badd, n1, n2, n4);
 }

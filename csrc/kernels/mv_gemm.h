@@ -101,11 +101,7 @@ bool mv_wgrad256_3x3(const void* X, const void* DY, float* partial, int N, int H
                      int K, int stride, hipStream_t st);
 // Stride-2 3x3 (pad 1) data gradient on the same pipeline (AMODE 4, one launch per output
 // parity class): dy [Nb, H/2, W/2, Cout], wt = the transposed, flipped filter [Cin][3][3][Cout],
-// dx [Nb, H, W, Cin] (every pixel written); H, W even, Cin % 256 == 0.  bn_x + partial
-// (rows = mv_dgrad256_s2_partials): d = fma(bn_x, scale, bias) > 0 ? bf16(dx) : 0 is stored
-// with the producing BN+ReLU's backward-reduce partials (as mv_conv256's bn_x).
+// dx [Nb, H, W, Cin] (every pixel written); H, W even, Cin % 256 == 0.
 bool mv_dgrad256_s2_supported(int Nb, int H, int W, int Cin, int Cout);
-int64_t mv_dgrad256_s2_partials(int Nb, int H, int W, int Cin);
 bool mv_dgrad256_s2(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int Cin,
-                    int Cout, float* partial, const void* bn_x, const float* bn_vec,
-                    hipStream_t st);
+                    int Cout, hipStream_t st);

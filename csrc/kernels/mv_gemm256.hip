@@ -996,17 +996,10 @@ bool mv_dgrad256_s2_supported(int Nb, int H, int W, int Cin, int Cout) {
          (int64_t)Cin * 9 * Cout * 2 < (int64_t(1) << 32) && M * 4 < (int64_t(1) << 31);
 }
 
-int64_t mv_dgrad256_s2_partials(int Nb, int H, int W, int Cin) {
-  return 4 * mv_gemm256_partials((int64_t)Nb * (H / 2) * (W / 2), Cin);
-}
-
 bool mv_dgrad256_s2(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int Cin,
-                    int Cout, float* partial, const void* bn_x, const float* bn_vec,
-                    hipStream_t st) {
+                    int Cout, hipStream_t st) {
   using namespace mv::g256;
-  if (!mv_dgrad256_s2_supported(Nb, H, W, Cin, Cout) || (bn_x && !partial) ||
-      (!bn_x && partial))
-    return false;
+  if (!mv_dgrad256_s2_supported(Nb, H, W, Cin, Cout)) return false;
   Args a{};
   a.A = (const __bf16*)dy;
   a.B = (const __bf16*)wt;
@@ -1020,22 +1013,14 @@ bool mv_dgrad256_s2(const void* dy, const void* wt, void* dx, int Nb, int H, int
   a.Cin = Cout;
   a.Kb = 9 * Cout;
   a.ds = 2;
-  const int64_t prow = mv_gemm256_partials(a.M, Cin);
-  // the 4-tap class first: the later, shorter launches fill in behind it
+  // the 4-tap class first: the later, shorter launches fill in behind it.  (A BN-reduce
+  // epilogue here measured slower than the separate reduce pass: the BN-input reads of the
+  // scattered class rows are latency-bound, 683 -> 1081 us for ResNet-50's layer3 shape.)
   for (int c = 3; c >= 0; --c) {
     a.ph = c >> 1;
     a.pw = c & 1;
     a.K = (1 + a.ph) * (1 + a.pw) * Cout;
-    if (bn_x) {
-      a.xb = (const __bf16*)bn_x;
-      a.mean = bn_vec;
-      a.sc = bn_vec + 2 * Cin;
-      a.bi = bn_vec + 3 * Cin;
-      a.partial = partial + (int64_t)(3 - c) * prow * 2 * Cin;
-      g256_launch<4, 4>(a, st);
-    } else {
-      g256_launch<0, 4>(a, st);
-    }
+    g256_launch<0, 4>(a, st);
   }
   return true;
 }

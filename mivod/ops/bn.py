@@ -62,7 +62,7 @@ def _fold_math(nat, wb, g, gram, vec, gamma, m, part, sdz, colsum, xs_fn, need_w
     the consumer's reduce partials (sum dz; or ``sdz`` given), ``colsum`` = [P, cin]
     column-sum partials of x or None (then ``xs_fn()`` gives colsum(x))."""
     cout, cin = g.shape
-    if _FOLD_MATH and part is not None:
+    if _FOLD_MATH and part is not None and cout % 64 == 0 and cin % 64 == 0:
         co, xsum = nat.fold_coeffs(part, wb, g, vec, gamma, m, colsum)
         if need_w and colsum is None:
             xsum = xs_fn().contiguous()

@@ -54,8 +54,7 @@ def dgrad1x1(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     gemm_ok = (dy.is_cuda and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
                and dy.is_contiguous(memory_format=torch.channels_last) and cout % 64 == 0
                and cin % 64 == 0)
-    if (gemm_ok and os.environ.get("MIVOD_DGRAD1X1_STREAM", "1") != "0" and cin < 256
-            and cout in (64, 128, 256)):
+    if gemm_ok and cin < 256 and cout in (64, 128, 256):
         from . import kernels as K
         n, _, h, wd = dy.shape
         m = n * h * wd
@@ -296,13 +295,6 @@ def _dgrad_s2_on_mivod(cin: int, h: int, w: int) -> bool:
             and h % 2 == 0 and w % 2 == 0)
 
 
-def _dgrad_s2_bn(cin: int) -> bool:
-    """The producing BN+ReLU's backward reduce in the stride-2 data gradient's epilogue
-    (256 x 256 pipeline only).  Off by default: the epilogue's scattered BN-input reads are
-    latency-bound (micro: layer3 683 -> 1081 us, more than the separate reduce pass's
-    241 us); MIVOD_CONV3X3_DGRAD_S2_BN=1 turns it on."""
-    return os.environ.get("MIVOD_CONV3X3_DGRAD_S2_BN", "0") == "1" and cin % 256 == 0
-
 
 def _wgrad_on_mivod(cin: int, cout: int, stride: int) -> bool:
     """mivod's 3x3 weight-gradient kernel (csrc/kernels/mv_conv.hip wgrad3x3_kernel) beats
@@ -326,7 +318,7 @@ class _Conv3x3(torch.autograd.Function):
     backward reduce in its epilogue and hands (d, partials) to it through the slot, the
     same protocol as ``_Conv1x1BN``; the weight gradient on mivod's wgrad3x3 kernel
     (MIOpen for the 512-channel stride-2 conv); stride-2 data gradient on mv_gemm256's
-    parity-class GEMMs (even input size; optionally with the BN+ReLU reduce), else MIOpen."""
+    parity-class GEMMs (even input size), else MIOpen."""
 
     @staticmethod
     def forward(ctx, x, w, stride, shift, stats, slot):
@@ -379,17 +371,9 @@ class _Conv3x3(torch.autograd.Function):
             r = []
             if need_x and s == 2 and _dgrad_s2_on_mivod(w.shape[1], x.shape[2], x.shape[3]):
                 from . import kernels as K
-                wt = _transposed_filter(w)
-                if (slot is not None and slot.bn is not None and slot.mode == 1
-                        and slot.pending is None):
-                    xb, _, vec = slot.bn
-                    r = K.native().conv3x3_s2_dgrad(dy, wt, x.shape[2], x.shape[3], xb, vec)
-                    if r:
-                        slot.pending = (r[0], r[1])
-                else:
-                    r = K.native().conv3x3_s2_dgrad(dy, wt, x.shape[2], x.shape[3])
-                    if r:
-                        dx = r[0]
+                r = K.native().conv3x3_s2_dgrad(dy, _transposed_filter(w), x.shape[2], x.shape[3])
+                if r:
+                    dx = r[0]
             if need_x and not r:
                 dx, _, _ = torch.ops.aten.convolution_backward(
                     dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])
@@ -415,9 +399,9 @@ def bwd3x3_fusable(m: nn.Conv2d, x: torch.Tensor):
         return None
     if m.stride[0] == 1 and _dgrad_on_mivod(m.in_channels, m.out_channels):
         return slot
-    if (m.stride[0] == 2 and _dgrad_s2_on_mivod(m.in_channels, x.shape[2], x.shape[3])
-            and _dgrad_s2_bn(m.in_channels)):
-        return slot
+    # (stride 2: a BN-reduce epilogue on the parity-class GEMMs measured slower than the
+    # separate reduce pass — its scattered BN-input reads are latency-bound, 683 -> 1081 us
+    # for the layer3 shape — so the producing BN keeps its own reduce there)
     return None
 
 

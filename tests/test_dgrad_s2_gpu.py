@@ -1,6 +1,6 @@
-"""Stride-2 3x3 data gradient on mv_gemm256's parity-class gather GEMMs (csrc/kernels/
-mv_gemm256.hip AMODE 4) against an fp32 PyTorch reference, with and without the producing
-BN+ReLU's backward reduce in the epilogue, and through the ResNet conv path."""
+"""Stride-2 3x3 data gradient as output-parity-class gather GEMMs (csrc/kernels/
+mv_gemm256.hip AMODE 4, mv_conv.hip conv3x3_kernel DG) against an fp32 PyTorch reference,
+and through the ResNet conv path."""
 import copy
 
 import pytest
@@ -54,34 +54,9 @@ def test_dgrad_s2_matches_fp32(cuda, n, c, k, h, w):
     torch.testing.assert_close(dx.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
 
 
-@pytest.mark.parametrize("n,c,k,h,w", _SHAPES[:5])
-def test_dgrad_s2_bn_reduce_matches_reference(cuda, n, c, k, h, w):
-    nat = _nat()
-    g = torch.Generator(device=cuda).manual_seed(7 * n + c + k + w)
-    dy = _cl(torch.randn(n, k, h // 2, w // 2, device=cuda, generator=g).to(torch.bfloat16))
-    wgt = (torch.randn(k, c, 3, 3, device=cuda, generator=g) / (9 * k) ** 0.5).to(torch.bfloat16)
-    xb = _cl(torch.randn(n, c, h, w, device=cuda, generator=g).to(torch.bfloat16))
-    vec = torch.randn(4, c, device=cuda, generator=g)
-    d, part = nat.conv3x3_s2_dgrad(dy, _wt(wgt), h, w, xb, vec)
-    dg = _ref_dx(dy, wgt, h, w).to(torch.bfloat16).float()
-    on = (xb.float() * vec[2].view(1, -1, 1, 1) + vec[3].view(1, -1, 1, 1)) > 0
-    ref = torch.where(on, dg, torch.zeros_like(dg))
-    torch.testing.assert_close(d.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
-    rr = ref.permute(0, 2, 3, 1).reshape(-1, c)
-    xr = xb.float().permute(0, 2, 3, 1).reshape(-1, c)
-    assert torch.isfinite(part).all()
-    sm = part.sum(0)
-    torch.testing.assert_close(sm[0], rr.sum(0), rtol=2e-2, atol=0.5)
-    torch.testing.assert_close(sm[1], (rr * (xr - vec[0])).sum(0), rtol=2e-2, atol=1.0)
-
-
 def test_dgrad_s2_declines_uncovered_shapes(cuda):
     nat = _nat()
     dy = _cl(torch.zeros(1, 64, 4, 4, device=cuda, dtype=torch.bfloat16))
-    w128 = torch.zeros(64, 128, 3, 3, device=cuda, dtype=torch.bfloat16)
-    xb = _cl(torch.zeros(1, 128, 8, 8, device=cuda, dtype=torch.bfloat16))
-    vec = torch.zeros(4, 128, device=cuda)
-    assert nat.conv3x3_s2_dgrad(dy, _wt(w128), 8, 8, xb, vec) == []   # BN: % 256 only
     w32 = torch.zeros(64, 32, 3, 3, device=cuda, dtype=torch.bfloat16)
     assert nat.conv3x3_s2_dgrad(dy, _wt(w32), 8, 8) == []       # dx channels % 64 != 0
     w256 = torch.zeros(64, 256, 3, 3, device=cuda, dtype=torch.bfloat16)
@@ -90,13 +65,10 @@ def test_dgrad_s2_declines_uncovered_shapes(cuda):
         nat.conv3x3_s2_dgrad(dy, _wt(w256), 12, 12)             # does not match dy
 
 
-@pytest.mark.parametrize("c,h,fuse", [(256, 14, "1"), (512, 8, "1"), (256, 14, "0"),
-                                      (128, 16, "0")])
-def test_conv_bn_s2_backward_matches_miopen(cuda, monkeypatch, c, h, fuse):
-    """BN+ReLU -> stride-2 3x3 conv -> BN: the parity-class data gradient (with BN1's reduce
-    fused when asked: BN1 takes it through its slot) == MIOpen's backward-data + BN1's own
-    reduce."""
-    monkeypatch.setenv("MIVOD_CONV3X3_DGRAD_S2_BN", fuse)
+@pytest.mark.parametrize("c,h", [(256, 14), (512, 8), (128, 16)])
+def test_conv_bn_s2_backward_matches_miopen(cuda, monkeypatch, c, h):
+    """BN+ReLU -> stride-2 3x3 conv -> BN: the parity-class data gradient == MIOpen's
+    backward-data (the whole chain's input, weight and BN-parameter gradients)."""
     from mivod.ops.bn import BatchNorm2d, conv_bn
     from mivod.ops.conv import Conv2d
     torch.manual_seed(0)
@@ -121,11 +93,8 @@ def test_conv_bn_s2_backward_matches_miopen(cuda, monkeypatch, c, h, fuse):
         torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2 * float(b.abs().max()))
 
 
-@pytest.mark.parametrize("fuse", ["0", "1"])
-def test_resnet_uses_dgrad_s2(cuda, monkeypatch, fuse):
-    """Every stride-2 conv2 takes the parity-class kernels in a ResNet backward (with BN1's
-    reduce when MIVOD_CONV3X3_DGRAD_S2_BN=1 and >= 256 channels)."""
-    monkeypatch.setenv("MIVOD_CONV3X3_DGRAD_S2_BN", fuse)
+def test_resnet_uses_dgrad_s2(cuda, monkeypatch):
+    """Every stride-2 conv2 takes the parity-class kernels in a ResNet backward."""
     from mivod.models.resnet import ResNet, to_mixed_bf16
     nat = _nat()
     calls = []
@@ -133,7 +102,7 @@ def test_resnet_uses_dgrad_s2(cuda, monkeypatch, fuse):
 
     def counted(*a):
         r = real(*a)
-        calls.append((a[1].shape[0], len(a) > 4, len(r)))
+        calls.append((a[1].shape[0], len(r)))
         return r
 
     monkeypatch.setattr(nat, "conv3x3_s2_dgrad", counted)
@@ -142,5 +111,4 @@ def test_resnet_uses_dgrad_s2(cuda, monkeypatch, fuse):
     x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
     F.cross_entropy(m(x).float(), torch.randint(0, 10, (4,), device=cuda)).backward()
     # layer2.0 (128 ch, 16x16 -> 8x8), layer3.0 (256 ch, 8x8 -> 4x4), layer4.0 (512 ch)
-    f = fuse == "1"
-    assert sorted(calls) == [(128, False, 1), (256, f, 2 if f else 1), (512, f, 2 if f else 1)], calls
+    assert sorted(calls) == [(128, 1), (256, 1), (512, 1)], calls

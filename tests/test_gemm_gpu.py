@@ -736,7 +736,7 @@ def test_gemm_nt_apply_dual_matches_materialised(cuda, M, N):
     assert torch.equal(y1, y2) and torch.equal(m1, m2)
 
 
-@pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256)])
+@pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256), (2048, 512), (256, 512)])
 @pytest.mark.parametrize("colsum", [True, False])
 def test_fold_math_kernels_match_eager(cuda, monkeypatch, cout, cin, colsum):
     """mv_fold.hip's two kernels == the eager PyTorch composition of the fold's small math."""
