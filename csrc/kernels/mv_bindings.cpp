@@ -1565,6 +1565,69 @@ std::vector<at::Tensor> conv3x3_s2_dgrad(at::Tensor dy, at::Tensor wt, int64_t H
   return {dx};
 }
 
+// Data-gradient filters of many convs in one launch: for every channels_last bf16 w
+// [K, C, ks, ks] the channels_last [C, K, ks, ks] filter with the taps rotated 180 degrees
+// (w.transpose(0, 1).flip(2, 3); for 1x1 W^T).  Outputs and the device block table are
+// cached per input set (the filters live in the optimizer's arena: stable pointers), so a
+// step costs one kernel.
+std::vector<at::Tensor> transpose_filters(std::vector<at::Tensor> ws) {
+  struct Entry {
+    std::vector<const void*> src;
+    std::vector<at::Tensor> outs;
+    at::Tensor table;
+    int64_t blocks = 0;
+  };
+  // (heap-allocated and never destroyed: tensors must not be freed after the HIP runtime at
+  // process exit)
+  static std::vector<Entry>& cache = *new std::vector<Entry>();
+  TORCH_CHECK(!ws.empty(), "transpose_filters: no filters");
+  const int n = (int)ws.size();
+  std::vector<const void*> src(n);
+  std::vector<int> K(n), C(n), ks(n);
+  for (int i = 0; i < n; ++i) {
+    const at::Tensor& w = ws[i];
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 &&
+                    w.size(2) == w.size(3) && w.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    w.device() == ws[0].device(),
+                "transpose_filters: filters must be channels_last bf16 [K, C, k, k] on one GPU");
+    src[i] = w.data_ptr();
+    K[i] = (int)w.size(0);
+    C[i] = (int)w.size(1);
+    ks[i] = (int)w.size(2);
+  }
+  c10::DeviceGuard guard(ws[0].device());
+  Entry* e = nullptr;
+  for (auto& c : cache) {
+    if (c.src != src || (int)c.outs.size() != n) continue;
+    bool same = true;
+    for (int i = 0; i < n && same; ++i)
+      same = c.outs[i].size(0) == C[i] && c.outs[i].size(1) == K[i] && c.outs[i].size(2) == ks[i] &&
+             c.outs[i].device() == ws[i].device();
+    if (same) { e = &c; break; }
+  }
+  if (!e) {
+    if (cache.size() >= 8) cache.erase(cache.begin());
+    Entry ne;
+    ne.src = src;
+    std::vector<void*> dst(n);
+    for (int i = 0; i < n; ++i) {
+      ne.outs.push_back(at::empty({C[i], K[i], ks[i], ks[i]}, ws[i].options(),
+                                  at::MemoryFormat::ChannelsLast));
+      dst[i] = ne.outs[i].data_ptr();
+    }
+    ne.blocks = mv_transpose_filters_blocks(K.data(), C.data(), ks.data(), n);
+    const int64_t bytes = mv_transpose_filters_table_bytes(n, ne.blocks);
+    at::Tensor host = at::empty({bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+    mv_transpose_filters_table(src.data(), dst.data(), K.data(), C.data(), ks.data(), n,
+                               host.data_ptr());
+    ne.table = host.to(ws[0].device(), /*non_blocking=*/false);
+    cache.push_back(std::move(ne));
+    e = &cache.back();
+  }
+  mv_transpose_filters(e->table.data_ptr(), n, e->blocks, cur_stream());
+  return e->outs;
+}
+
 // weight gradient of y = conv3x3(x, w, stride, pad 1): dw [K, C, 3, 3] channels_last bf16
 at::Tensor wgrad3x3(at::Tensor x, at::Tensor dy, int64_t stride,
                     c10::optional<at::Tensor> in_scale, c10::optional<at::Tensor> in_bias) {
@@ -1754,6 +1817,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("wgrad1x1", &wgrad1x1, "1x1 (pad 0, stride 1/2) conv weight gradient on MFMA",
         py::arg("x"), py::arg("dy"), py::arg("stride") = 1, py::arg("fp32_out") = false,
         py::arg("dy2") = py::none());
+  m.def("transpose_filters", &transpose_filters,
+        "data-gradient filters (transposed, taps rotated) of many convs in one launch");
   m.def("wgrad3x3", &wgrad3x3, "3x3 (pad 1) conv weight gradient on MFMA (transposed LDS reads)",
         py::arg("x"), py::arg("dy"), py::arg("stride") = 1, py::arg("in_scale") = py::none(),
         py::arg("in_bias") = py::none());

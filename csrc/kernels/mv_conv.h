@@ -69,3 +69,13 @@ bool mv_wgrad64(const void* x, const void* dy, float* partial, int grid, int N, 
 bool mv_conv3x3_s2_dgrad_supported(int Nb, int H, int W, int C, int K);
 bool mv_conv3x3_s2_dgrad(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C,
                          int K, hipStream_t st);
+
+// The data-gradient filters of n convs in one launch (see mv_conv.hip): w [K][ks][ks][C] ->
+// wt [C][ks][ks][K], taps rotated.  The caller builds the table once (host image of
+// mv_transpose_filters_table_bytes bytes, copied to device memory) and reuses it while the
+// filter and output pointers stay put.
+int64_t mv_transpose_filters_blocks(const int* K, const int* C, const int* ks, int n);
+int64_t mv_transpose_filters_table_bytes(int n, int64_t blocks);
+void mv_transpose_filters_table(const void* const* src, void* const* dst, const int* K,
+                                const int* C, const int* ks, int n, void* host_image);
+void mv_transpose_filters(const void* table, int n, int64_t blocks, hipStream_t st);

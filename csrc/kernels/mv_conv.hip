@@ -509,6 +509,79 @@ bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, in
   return true;
 }
 
+// Data-gradient filters of many convs in ONE launch: each w [K][ks][ks][C] (a channels_last
+// [K, C, ks, ks] filter) -> wt [C][ks][ks][K] with the taps rotated 180 degrees (the
+// channels_last [C, K, ks, ks] filter of dX = conv(dY, wt); for ks = 1 plain W^T).  A block
+// transposes one 64 (k) x 64 (c) tile of one tap through LDS (both sides coalesced); the
+// block table (tensor, tap, k0, c0) is built on the host.  Replaces a flip + layout copy
+// (or a transpose copy) per conv per step: ~55 small PyTorch launches at ResNet-50.
+namespace mv {
+namespace conv {
+struct TfTensor {
+  const __bf16* src;
+  __bf16* dst;
+  int K, C, ks;
+};
+struct TfBlock {
+  int t, tap, k0, c0;
+};
+__global__ __launch_bounds__(256) void transpose_filters_kernel(const TfTensor* __restrict__ ts,
+                                                                const TfBlock* __restrict__ bl) {
+  __shared__ __bf16 tile[64][66];
+  const TfBlock b = bl[blockIdx.x];
+  const TfTensor tt = ts[b.t];
+  const int ks = tt.ks, taps = ks * ks;
+  const int r = b.tap / ks, s = b.tap - r * ks;
+  const int ftap = (ks - 1 - r) * ks + (ks - 1 - s);   // source tap (rotated)
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {                   // read rows k, c contiguous
+    const int k = b.k0 + i, c = b.c0 + tx;
+    tile[i][tx] = (k < tt.K && c < tt.C) ? tt.src[((int64_t)k * taps + ftap) * tt.C + c]
+                                         : (__bf16)0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {                   // write rows c, k contiguous
+    const int c = b.c0 + i, k = b.k0 + tx;
+    if (c < tt.C && k < tt.K) tt.dst[((int64_t)c * taps + b.tap) * tt.K + k] = tile[tx][i];
+  }
+}
+}  // namespace conv
+}  // namespace mv
+
+int64_t mv_transpose_filters_blocks(const int* K, const int* C, const int* ks, int n) {
+  int64_t nb = 0;
+  for (int i = 0; i < n; ++i)
+    nb += (int64_t)ks[i] * ks[i] * ((K[i] + 63) / 64) * ((C[i] + 63) / 64);
+  return nb;
+}
+
+// table: device memory of n TfTensor (32 bytes each) followed by the block list (16 bytes
+// each), written by the caller from mv_transpose_filters_table's host image
+void mv_transpose_filters_table(const void* const* src, void* const* dst, const int* K,
+                                const int* C, const int* ks, int n, void* host_image) {
+  using namespace mv::conv;
+  TfTensor* ts = reinterpret_cast<TfTensor*>(host_image);
+  TfBlock* bl = reinterpret_cast<TfBlock*>(ts + n);
+  int64_t j = 0;
+  for (int i = 0; i < n; ++i) {
+    ts[i] = TfTensor{(const __bf16*)src[i], (__bf16*)dst[i], K[i], C[i], ks[i]};
+    for (int tap = 0; tap < ks[i] * ks[i]; ++tap)
+      for (int k0 = 0; k0 < K[i]; k0 += 64)
+        for (int c0 = 0; c0 < C[i]; c0 += 64) bl[j++] = TfBlock{i, tap, k0, c0};
+  }
+}
+
+int64_t mv_transpose_filters_table_bytes(int n, int64_t blocks) {
+  return (int64_t)n * (int64_t)sizeof(mv::conv::TfTensor) + blocks * (int64_t)sizeof(mv::conv::TfBlock);
+}
+
+void mv_transpose_filters(const void* table, int n, int64_t blocks, hipStream_t st) {
+  using namespace mv::conv;
+  const TfTensor* ts = reinterpret_cast<const TfTensor*>(table);
+  const TfBlock* bl = reinterpret_cast<const TfBlock*>(ts + n);
+  hipLaunchKernelGGL(transpose_filters_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ts, bl);
+}
+
 // Stride-2 3x3 (pad 1) data gradient: dx [Nb, H, W, C] from dy [Nb, H/2, W/2, K] and the
 // transposed flipped filter wt [C][3][3][K]; four parity-class launches (DG), every dx pixel
 // written once.  C % 256 == 0 goes to mv_gemm256.hip's AMODE 4, else conv3x3_kernel.

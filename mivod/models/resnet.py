@@ -16,7 +16,8 @@ import os
 
 import torch.nn.functional as F
 
-from ..ops.conv import Conv2d, conv1x1_stats, stats_fusable
+from ..ops.conv import (Conv2d, conv1x1_stats, end_dgrad_filters, prepare_dgrad_filters,
+                        stats_fusable)
 from ..ops import bn as _bn
 from ..ops.bn import (BatchNorm2d, bn_relu_conv3x3, bn_relu_maxpool, conv_bn, downsample_tap,
                       global_avg_pool, pad_channels, shortcut_foldable, shortcut_fusable, tap)
@@ -196,7 +197,33 @@ class ResNet(nn.Module):
             layers.append(Bottleneck(self.inplanes, planes, zero_init_residual=zir))
         return nn.Sequential(*layers)
 
+    def _dgrad_convs(self):
+        """The convs whose data-gradient filters backward uses (every Conv2d but the stem),
+        when they are channels_last bf16 GPU filters; else []."""
+        cv = getattr(self, "_mv_dgrad_convs", None)
+        if cv is None:
+            cv = [m for m in self.modules() if isinstance(m, nn.Conv2d)
+                  and not isinstance(m, StemConv) and m.groups == 1]
+            self._mv_dgrad_convs = cv
+        ok = all(m.weight.is_cuda and m.weight.dtype == torch.bfloat16
+                 and m.weight.is_contiguous(memory_format=torch.channels_last) for m in cv)
+        return cv if ok else []
+
     def forward(self, x):
+        prepared = False
+        if self.training and torch.is_grad_enabled() and x.is_cuda:
+            convs = self._dgrad_convs()
+            if convs:
+                # all data-gradient filters of this step in one launch (ops.conv)
+                prepare_dgrad_filters(convs)
+                prepared = True
+        try:
+            return self._forward(x)
+        finally:
+            if prepared:
+                end_dgrad_filters()
+
+    def _forward(self, x):
         r = None
         if self.bn1.training and self.bn1.track_running_stats:
             r = self.conv1.forward_stats(x, self.bn1.running_mean)

@@ -176,6 +176,8 @@ class _DownsampleTapConv(torch.autograd.Function):
     def forward(ctx, x, w, s, slot, shift=None):
         ctx.save_for_backward(x, w)
         ctx.s, ctx.slot = s, slot
+        from .conv import dgrad_filter
+        ctx.wt = dgrad_filter(w)
         # the strided 1x1 conv on the 256 x 256 GEMM (rows gathered at the stride) with the
         # following BN's statistics in its epilogue, when it covers the shape
         r = K.native().conv1x1_strided_stats(x, w, s, shift) if _GEMM256 else None
@@ -197,7 +199,7 @@ class _DownsampleTapConv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             from .conv import dgrad1x1
             assert ctx.slot.grad is None, "a tapped output has one shortcut consumer"
-            ctx.slot.grad = dgrad1x1(dy, w).contiguous(memory_format=torch.channels_last)
+            ctx.slot.grad = dgrad1x1(dy, w, ctx.wt).contiguous(memory_format=torch.channels_last)
             ctx.slot.stride = ctx.s
             ctx.slot.full_shape = x.shape
         if ctx.needs_input_grad[1]:
@@ -631,6 +633,8 @@ class _Conv1x1BNFold(torch.autograd.Function):
         ctx.save_for_backward(x, w, z, keep, vec, weight, vec_r, res_w,
                               residual if vec_r is not None else None, res_conv_w)
         ctx.slot = slot
+        from .conv import dgrad_filter
+        ctx.wt = dgrad_filter(w)
         ctx.xslot = getattr(x, "_mv_slot", None)     # x = relu(bn2(z2)): BN2's GradSlot
         ctx.colsum = getattr(ctx.xslot, "colsum", None)
         slot.bn = (z, keep, vec)
@@ -702,7 +706,7 @@ class _Conv1x1BNFold(torch.autograd.Function):
                 dy2, s2 = slot.take_strided()
                 dlz, dg, db, dz = nat.bn_bwd(3, dy, z, keep, vec, weight, True, dy2, s2)
             if need_x:
-                dx = dgrad1x1(dlz, w)
+                dx = dgrad1x1(dlz, w, ctx.wt)
             if need_w:
                 dw = wgrad1x1(dlz, x, w)
         dres = dz if ctx.needs_input_grad[8] else None
@@ -792,6 +796,8 @@ class _BNReluConv64(torch.autograd.Function):
         z2 = nat.conv3x3(z1, w2.contiguous(memory_format=torch.channels_last), 1, shift2, part2,
                          vec1[2], vec1[3])
         ctx.save_for_backward(z1, vec1, g1, w2)
+        from .conv import dgrad_filter
+        ctx.wt = dgrad_filter(w2)
         ctx.mark_non_differentiable(part2)
         ctx.set_materialize_grads(False)
         return z2, part2
@@ -800,12 +806,12 @@ class _BNReluConv64(torch.autograd.Function):
     def backward(ctx, dz2, _dpart):
         if dz2 is None:
             return (None,) * 10
-        from .conv import _transposed_filter
+        from .conv import _wt_or_make
         z1, vec1, g1, w2 = ctx.saved_tensors
         nat = K.native()
         dz2 = _cl(dz2)
         # conv2's data gradient with BN1's ReLU mask and backward reduce in its epilogue
-        d1, p1 = nat.conv3x3_bn_bwd(dz2, _transposed_filter(w2), z1, vec1)
+        d1, p1 = nat.conv3x3_bn_bwd(dz2, _wt_or_make(w2, ctx.wt), z1, vec1)
         dw2 = (nat.wgrad3x3(z1, dz2, 1, vec1[2], vec1[3]) if ctx.needs_input_grad[8] else None)
         need_aff = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
         dz1, dg1, db1 = nat.bn_bwd_from_partials(d1, z1, vec1, g1, need_aff, p1)

@@ -44,7 +44,45 @@ def _transposed_filter(w: torch.Tensor) -> torch.Tensor:
     return wt.contiguous(memory_format=torch.channels_last)
 
 
-def dgrad1x1(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+# Data-gradient filters of a whole model, made in ONE launch at the start of its training
+# forward (``prepare_dgrad_filters``; csrc/kernels/mv_conv.hip transpose_filters_kernel)
+# instead of a flip + layout copy / transpose copy per conv in backward (~55 launches per
+# ResNet-50 step).  The map is live only inside that forward: an autograd function looks
+# its filter up at FORWARD time and keeps it in ctx, so its backward uses exactly the
+# filter of the weights it ran with.  (The buffers are reused by the next prepared
+# forward: a graph kept across an optimizer step and a new forward would see the new
+# weights' filters.)
+_DGRAD_FILTERS: dict = {}
+
+
+def prepare_dgrad_filters(convs) -> None:
+    """Transposed, tap-rotated filters of ``convs`` (channels_last bf16 GPU Conv2d modules)
+    in one launch; ``end_dgrad_filters()`` closes the window."""
+    from . import kernels as K
+    ws = [m.weight for m in convs]
+    _DGRAD_FILTERS.clear()
+    if not ws or os.environ.get("MIVOD_DGRAD_FILTERS", "1") == "0":
+        return
+    for w, wt in zip(ws, K.native().transpose_filters(ws)):
+        _DGRAD_FILTERS[(w.data_ptr(), tuple(w.shape))] = wt
+
+
+def end_dgrad_filters() -> None:
+    _DGRAD_FILTERS.clear()
+
+
+def dgrad_filter(w: torch.Tensor):
+    """The prepared data-gradient filter of w ([C, K, k, k] channels_last) or None."""
+    if not _DGRAD_FILTERS:
+        return None
+    return _DGRAD_FILTERS.get((w.data_ptr(), tuple(w.shape)))
+
+
+def _wt_or_make(w: torch.Tensor, wt):
+    return wt if wt is not None else _transposed_filter(w)
+
+
+def dgrad1x1(dy: torch.Tensor, w: torch.Tensor, wt=None) -> torch.Tensor:
     """Input gradient of a stride-1 1x1 conv, dX = dY . W as an NHWC GEMM: mivod's
     256 x 256 kernel (mv_gemm256.hip) when Cin % 256 == 0 and Cout >= 256, mv_gemm's
     streaming kernel for Cout in {64, 128, 256} (ResNet-50 layer1.0's 64 -> 64 conv1: CK's
@@ -54,13 +92,14 @@ def dgrad1x1(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     gemm_ok = (dy.is_cuda and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
                and dy.is_contiguous(memory_format=torch.channels_last) and cout % 64 == 0
                and cin % 64 == 0)
+    # (wt: the prepared [cin, cout, 1, 1] channels_last transpose = W^T as [cin, cout])
+    wt2 = wt.reshape(cin, cout) if wt is not None else w.reshape(cout, cin).t().contiguous()
     if gemm_ok and cin < 256 and cout in (64, 128, 256):
         from . import kernels as K
         n, _, h, wd = dy.shape
         m = n * h * wd
         dx = torch.empty(m, cin, dtype=dy.dtype, device=dy.device)
-        K.native().gemm_nt(dy.permute(0, 2, 3, 1).reshape(m, cout),
-                           w.reshape(cout, cin).t().contiguous(), dx, None, None)
+        K.native().gemm_nt(dy.permute(0, 2, 3, 1).reshape(m, cout), wt2, dx, None, None)
         return dx.view(n, h, wd, cin).permute(0, 3, 1, 2)
     if (gemm_ok and os.environ.get("MIVOD_GEMM256", "1") != "0" and cin % 256 == 0
             and cout >= 256):
@@ -68,10 +107,9 @@ def dgrad1x1(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         n, _, h, wd = dy.shape
         m = n * h * wd
         dx = torch.empty(m, cin, dtype=dy.dtype, device=dy.device)
-        K.native().gemm_nt(dy.permute(0, 2, 3, 1).reshape(m, cout),
-                           w.reshape(cout, cin).t().contiguous(), dx, None, None)
+        K.native().gemm_nt(dy.permute(0, 2, 3, 1).reshape(m, cout), wt2, dx, None, None)
         return dx.view(n, h, wd, cin).permute(0, 3, 1, 2)
-    return F.conv2d(dy, _transposed_filter(w))
+    return F.conv2d(dy, _wt_or_make(w, wt))
 
 
 def _wgrad1x1_on_mivod(cin: int, cout: int) -> bool:
@@ -100,6 +138,7 @@ class _ConvDgradFwd(torch.autograd.Function):
     def forward(ctx, x, w, pad):
         ctx.save_for_backward(x, w)
         ctx.pad = pad
+        ctx.wt = dgrad_filter(w)
         return F.conv2d(x, w, None, 1, pad)
 
     @staticmethod
@@ -108,8 +147,8 @@ class _ConvDgradFwd(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = (dgrad1x1(dy, w) if w.shape[2] == 1 and w.shape[3] == 1
-                  else F.conv2d(dy, _transposed_filter(w), None, 1, ctx.pad))
+            dx = (dgrad1x1(dy, w, ctx.wt) if w.shape[2] == 1 and w.shape[3] == 1
+                  else F.conv2d(dy, _wt_or_make(w, ctx.wt), None, 1, ctx.pad))
         if ctx.needs_input_grad[1]:
             if w.shape[2] == 1 and w.shape[3] == 1:
                 dw = wgrad1x1(dy, x, w)
@@ -168,6 +207,7 @@ class _Conv1x1BN(torch.autograd.Function):
             part = torch.empty(0, dtype=torch.float32, device=x.device)
         ctx.save_for_backward(x, w)
         ctx.slot = slot
+        ctx.wt = dgrad_filter(w)
         ctx.mark_non_differentiable(part)
         # no zero-filled gradient for the statistics output (a fill kernel per call)
         ctx.set_materialize_grads(False)
@@ -190,14 +230,16 @@ class _Conv1x1BN(torch.autograd.Function):
                 xb, mask, vec = slot.bn
                 dz = torch.empty_like(x)
                 g2, s2 = slot.take_strided()      # stride > 1: a stage-entry shortcut's grid
+                wt2 = (ctx.wt.reshape(cin, cout) if ctx.wt is not None
+                       else w.reshape(cout, cin).t().contiguous())
                 part = K.native().gemm_nt_bn_bwd(
-                    dy.permute(0, 2, 3, 1).reshape(m, cout), w.reshape(cout, cin).t().contiguous(),
+                    dy.permute(0, 2, 3, 1).reshape(m, cout), wt2,
                     dz.permute(0, 2, 3, 1).reshape(m, cin), g2, mask,
                     None if slot.fold else xb.permute(0, 2, 3, 1).reshape(m, cin), vec, 0, s2,
                     h, wd)
                 slot.pending = (dz, part)
             else:
-                dx = dgrad1x1(dy, w)
+                dx = dgrad1x1(dy, w, ctx.wt)
         if ctx.needs_input_grad[1]:
             dw = wgrad1x1(dy, x, w)
         return dx, dw, None, None, None
@@ -338,6 +380,7 @@ class _Conv3x3(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.stride = stride
         ctx.slot = slot
+        ctx.wt = dgrad_filter(w)
         ctx.mark_non_differentiable(part)
         # no zero-filled gradient for the statistics output (a fill kernel per call)
         ctx.set_materialize_grads(False)
@@ -355,7 +398,7 @@ class _Conv3x3(torch.autograd.Function):
         dx = dw = None
         if s == 1:
             if need_x:
-                wt = _transposed_filter(w)
+                wt = _wt_or_make(w, ctx.wt)
                 if _dgrad_on_mivod(w.shape[1], w.shape[0]):
                     from . import kernels as K
                     if (slot is not None and slot.bn is not None and slot.mode == 1
@@ -371,7 +414,8 @@ class _Conv3x3(torch.autograd.Function):
             r = []
             if need_x and s == 2 and _dgrad_s2_on_mivod(w.shape[1], x.shape[2], x.shape[3]):
                 from . import kernels as K
-                r = K.native().conv3x3_s2_dgrad(dy, _transposed_filter(w), x.shape[2], x.shape[3])
+                r = K.native().conv3x3_s2_dgrad(dy, _wt_or_make(w, ctx.wt), x.shape[2],
+                                                x.shape[3])
                 if r:
                     dx = r[0]
             if need_x and not r:

@@ -408,3 +408,49 @@ def test_stem_kernels_read_rgb_directly(cuda, n):
     assert torch.equal(z3, z4) and torch.equal(p3, p4)
     dz = _cl(torch.randn(n, 64, 112, 112, device=cuda, generator=g).to(torch.bfloat16))
     assert torch.equal(nat.stem_wgrad(x3, dz), nat.stem_wgrad(x4, dz))
+
+
+def test_transpose_filters_matches_torch(cuda):
+    """The one-launch data-gradient filters == w.transpose(0, 1).flip(2, 3) for every
+    filter (3x3 and 1x1, channel counts off the 64-tile grid), repeated calls reuse the
+    cached outputs and follow the current weights."""
+    nat = _nat()
+    g = torch.Generator(device=cuda).manual_seed(3)
+    shapes = [(64, 64, 3), (256, 128, 1), (100, 72, 3), (2048, 512, 1), (3, 5, 7), (512, 512, 3)]
+    ws = [_cl(torch.randn(k, c, s, s, device=cuda, generator=g).to(torch.bfloat16))
+          for k, c, s in shapes]
+    for rnd in range(2):
+        outs = nat.transpose_filters(ws)
+        for w, o in zip(ws, outs):
+            ref = _cl(w.transpose(0, 1).flip(2, 3))
+            assert o.shape == ref.shape and o.is_contiguous(memory_format=torch.channels_last)
+            assert torch.equal(o, ref)
+        with torch.no_grad():
+            for w in ws:
+                w.mul_(-1.5)
+
+
+def test_resnet_prepared_dgrad_filters_bitwise(cuda, monkeypatch):
+    """Backward with the model-wide prepared filters == the per-conv transposes
+    (MIVOD_DGRAD_FILTERS=0: the filters are bitwise equal, the gradients agree to MIOpen's
+    run-to-run algorithm choice on the shapes it still runs), and the prepared map is
+    closed after the forward."""
+    import copy
+
+    from mivod.models.resnet import ResNet, to_mixed_bf16
+    from mivod.ops import conv as CV
+    torch.manual_seed(0)
+    base = to_mixed_bf16(ResNet((2, 1, 2, 1), num_classes=10)).to(cuda)
+    x = _cl(torch.rand(4, 3, 64, 64, device=cuda).to(torch.bfloat16))
+    tgt = torch.randint(0, 10, (4,), device=cuda)
+    res = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("MIVOD_DGRAD_FILTERS", on)
+        m = copy.deepcopy(base)
+        out = m(x)
+        assert not CV._DGRAD_FILTERS
+        F.cross_entropy(out.float(), tgt).backward()
+        res[on] = {k: p.grad for k, p in m.named_parameters()}
+    for k, v in res["0"].items():
+        torch.testing.assert_close(res["1"][k].float(), v.float(), rtol=1e-2,
+                                   atol=1e-2 * float(v.float().abs().max()), msg=k)
