@@ -91,6 +91,92 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restri
   *reinterpret_cast<u32x2*>(idx + t * 8) = u32x2{lo, hi};
 }
 
+// k = 3 with the BN affine + ReLU prologue (the ResNet stem): the same result and the same
+// first-maximum index as maxpool_fwd_kernel<3>, with ~half its VALU work (that kernel is
+// VALU-bound: ~980 instructions per wave-output, PMC 100% VALU-active).  The BN + ReLU
+// outputs are rounded to bf16 two channels per instruction (v_cvt_pk_bf16_f32); as
+// non-negative bf16 values their bit patterns order like unsigned integers, so pass 1 keeps
+// a packed u16 maximum and pass 2 finds the first window position holding it (the order
+// torch's max_pool2d uses).  Positions outside the image take no part.
+__global__ __launch_bounds__(256) void maxpool_fwd_bnrelu3_kernel(const __bf16* __restrict__ x,
+                                                                 const float* __restrict__ scale,
+                                                                 const float* __restrict__ bias,
+                                                                 __bf16* __restrict__ y,
+                                                                 uint8_t* __restrict__ idx,
+                                                                 PoolGeo g) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const int cv = g.C / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)g.N * g.OH * g.OW * cv;
+  if (t >= total) return;
+  const uint32_t t32 = (uint32_t)t, cv32 = (uint32_t)cv;
+  const uint32_t pix0 = t32 / cv32;
+  const int c = (int)(t32 - pix0 * cv32) * 8;
+  const uint32_t pw = pix0 / (uint32_t)g.OW;
+  const int ow = (int)(pix0 - pw * (uint32_t)g.OW);
+  const uint32_t ph = pw / (uint32_t)g.OH;
+  const int oh = (int)(pw - ph * (uint32_t)g.OH);
+  const int n = (int)ph;
+  float sc[8], bi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = scale[c + j]; bi[j] = bias[c + j]; }
+  const int h0 = oh * g.s - g.p, w0 = ow * g.s - g.p;
+  uint32_t a[9][4];                       // packed bf16 BN+ReLU outputs of the 9 positions
+  uint32_t vmask = 0;                     // bit pos: inside the image
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int pos = kh * 3 + kw, ih = h0 + kh, iw = w0 + kw;
+      const bool ok = ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (ok) v = *reinterpret_cast<const u32x4*>(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + c);
+      vmask |= (ok ? 1u : 0u) << pos;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float lo = fmaxf(__builtin_fmaf(__uint_as_float(v[q] << 16), sc[2 * q], bi[2 * q]), 0.f);
+        const float hi =
+            fmaxf(__builtin_fmaf(__uint_as_float(v[q] & 0xffff0000u), sc[2 * q + 1], bi[2 * q + 1]), 0.f);
+        a[pos][q] = ok ? cvt_pk_bf16(lo, hi) : 0u;
+      }
+    }
+  // pass 1: per-channel maximum of the bf16 bit patterns (packed unsigned 16-bit max)
+  u16x2 m[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) m[q] = __builtin_bit_cast(u16x2, a[0][q]);
+#pragma unroll
+  for (int pos = 1; pos < 9; ++pos)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      m[q] = __builtin_elementwise_max(m[q], __builtin_bit_cast(u16x2, a[pos][q]));
+  // pass 2: the first in-image position holding the maximum (scan backwards, keep the last
+  // assignment = the earliest position)
+  uint32_t arg[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) arg[j] = 0;
+#pragma unroll
+  for (int pos = 8; pos >= 0; --pos) {
+    if (!((vmask >> pos) & 1u)) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t mw = __builtin_bit_cast(uint32_t, m[q]);
+      const uint32_t d = a[pos][q] ^ mw;
+      if ((d & 0xffffu) == 0u) arg[2 * q] = (uint32_t)pos;
+      if ((d >> 16) == 0u) arg[2 * q + 1] = (uint32_t)pos;
+    }
+  }
+  typedef uint32_t u32x4s __attribute__((ext_vector_type(4)));
+  *reinterpret_cast<u32x4s*>(y + t * 8) = u32x4s{__builtin_bit_cast(uint32_t, m[0]),
+                                                 __builtin_bit_cast(uint32_t, m[1]),
+                                                 __builtin_bit_cast(uint32_t, m[2]),
+                                                 __builtin_bit_cast(uint32_t, m[3])};
+  const uint32_t lo = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+  const uint32_t hi = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  *reinterpret_cast<u32x2*>(idx + t * 8) = u32x2{lo, hi};
+}
+
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restrict__ dy,
                                                           const __bf16* __restrict__ dy2,
                                                           const uint8_t* __restrict__ idx,
@@ -394,7 +480,14 @@ void mv_maxpool_fwd(const void* x, const float* scale, const float* bias, bool r
   // (a 2x2-output-block variant, 25 loads per 4 outputs, measured level with this
   // per-output kernel at bs 2048 — 15,334 / 15,331 vs 15,319 / 15,344 img/s — and was
   // removed in round 3)
-  if (k == 3)
+  static const bool fast = [] {
+    const char* e = std::getenv("MIVOD_POOL_FWD_PACKED");
+    return !(e && e[0] == '0');
+  }();
+  if (k == 3 && relu && scale && bias && fast)
+    hipLaunchKernelGGL(maxpool_fwd_bnrelu3_kernel, dim3(blocks_for(total)), dim3(256), 0, st,
+                       (const __bf16*)x, scale, bias, (__bf16*)y, idx, g);
+  else if (k == 3)
     hipLaunchKernelGGL(maxpool_fwd_kernel<3>, dim3(blocks_for(total)), dim3(256), 0, st,
                        (const __bf16*)x, scale, bias, relu ? 1 : 0, (__bf16*)y, idx, g);
   else
