@@ -807,6 +807,27 @@ at::Tensor maxpool_bwd(at::Tensor dy, c10::optional<at::Tensor> dy2, at::Tensor 
   return dx;
 }
 
+// [5, C] fp32 {dgamma, dbeta, ca, cb, cc} of the BN+ReLU in front of a maxpool, from a reduce
+// over the pooled tensors (dy, dy2, the pooled output y); M = the BN's element rows
+static at::Tensor pool_bn_coefs(const at::Tensor& dy, const void* d2, const at::Tensor& y,
+                                const at::Tensor& vec, const c10::optional<at::Tensor>& gamma,
+                                int64_t M) {
+  const int64_t C = dy.size(1);
+  auto fo = dy.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({(int64_t)mv_pool_bn_partials(), 2, C}, fo);
+  mv_pool_bn_reduce(dy.data_ptr(), d2, y.data_ptr(), vec[0].data_ptr<float>(),
+                    vec[2].data_ptr<float>(), vec[3].data_ptr<float>(), part.data_ptr<float>(),
+                    dy.numel() / C, (int)C, cur_stream());
+  at::Tensor work = at::empty({5, C}, fo);
+  mv_bn_bwd_from_partials(nullptr, nullptr, nullptr, M, (int)C, vec[0].data_ptr<float>(),
+                          vec[1].data_ptr<float>(), opt_f32(gamma, C, "weight"),
+                          vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
+                          work[0].data_ptr<float>(), work[1].data_ptr<float>(),
+                          part.data_ptr<float>(), (int)part.size(0), work[2].data_ptr<float>(),
+                          work[3].data_ptr<float>(), work[4].data_ptr<float>(), cur_stream());
+  return work;
+}
+
 // {dx, dgamma, dbeta}: maxpool(3, 2, 1) backward fused with the backward of the BN+ReLU that
 // produced its input z (ResNet stem): y = the pooled output, vec = the BN's saved [4, C]
 std::vector<at::Tensor> maxpool_bn_bwd(at::Tensor dy, c10::optional<at::Tensor> dy2,
@@ -832,18 +853,7 @@ std::vector<at::Tensor> maxpool_bn_bwd(at::Tensor dy, c10::optional<at::Tensor> 
     d2 = dy2->data_ptr();
   }
   c10::DeviceGuard guard(dy.device());
-  auto fo = dy.options().dtype(at::kFloat);
-  at::Tensor part = at::empty({(int64_t)mv_pool_bn_partials(), 2, C}, fo);
-  mv_pool_bn_reduce(dy.data_ptr(), d2, y.data_ptr(), vec[0].data_ptr<float>(),
-                    vec[2].data_ptr<float>(), vec[3].data_ptr<float>(), part.data_ptr<float>(),
-                    N * OH * OW, (int)C, cur_stream());
-  at::Tensor work = at::empty({5, C}, fo);
-  mv_bn_bwd_from_partials(nullptr, nullptr, nullptr, N * H * W, (int)C, vec[0].data_ptr<float>(),
-                          vec[1].data_ptr<float>(), opt_f32(gamma, C, "weight"),
-                          vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
-                          work[0].data_ptr<float>(), work[1].data_ptr<float>(),
-                          part.data_ptr<float>(), (int)part.size(0), work[2].data_ptr<float>(),
-                          work[3].data_ptr<float>(), work[4].data_ptr<float>(), cur_stream());
+  at::Tensor work = pool_bn_coefs(dy, d2, y, vec, gamma, N * H * W);
   at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   TORCH_CHECK(mv_maxpool_bn_bwd(dy.data_ptr(), d2, idx.data_ptr<uint8_t>(), z.data_ptr(),
                                 vec[2].data_ptr<float>(), vec[3].data_ptr<float>(),
@@ -1204,6 +1214,54 @@ at::Tensor stem_wgrad(at::Tensor x, at::Tensor dz) {
   mv_stem_wgrad(x.data_ptr(), dz.data_ptr(), dw.data_ptr(), work.data_ptr<float>(), (int)N,
                 cur_stream(), (int)x.size(1));
   return dw;
+}
+
+// {dw, dgamma, dbeta}: the ResNet stem's maxpool + BN+ReLU backward and its conv's weight
+// gradient in one pass over the rows (mv_stem.hip, MvStemPoolBwd): the full-resolution dz is
+// never written.  x: the stem input, z: the conv output, y / idx: the pooled output and its
+// window argmax, vec: the BN's saved [4, 64]; dy (+ dy2): the pooled gradients.
+std::vector<at::Tensor> stem_wgrad_pool_bn(at::Tensor x, at::Tensor dy,
+                                           c10::optional<at::Tensor> dy2, at::Tensor idx,
+                                           at::Tensor y, at::Tensor z, at::Tensor vec,
+                                           c10::optional<at::Tensor> gamma) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  (x.size(1) == 4 || x.size(1) == 3) && x.size(2) == 224 && x.size(3) == 224 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_wgrad_pool_bn: x must be a channels_last bf16 [N, 3 or 4, 224, 224] GPU tensor");
+  const int64_t N = x.size(0);
+  check_nhwc(z, "z");
+  check_nhwc(dy, "dy");
+  check_nhwc(y, "y");
+  TORCH_CHECK(z.sizes() == at::IntArrayRef({N, 64, 112, 112}) && z.device() == x.device(),
+              "stem_wgrad_pool_bn: z must be [N, 64, 112, 112] on x's device");
+  TORCH_CHECK(dy.sizes() == at::IntArrayRef({N, 64, 56, 56}) && y.sizes() == dy.sizes() &&
+                  dy.device() == x.device() && y.device() == x.device(),
+              "stem_wgrad_pool_bn: dy / y must be [N, 64, 56, 56] on x's device");
+  TORCH_CHECK(idx.device() == x.device() && idx.scalar_type() == at::kByte &&
+                  idx.is_contiguous() && idx.numel() == dy.numel(),
+              "stem_wgrad_pool_bn: idx must be uint8 [N, 56, 56, 64]");
+  TORCH_CHECK(vec.device() == x.device() && vec.scalar_type() == at::kFloat &&
+                  vec.is_contiguous() && vec.numel() == 4 * 64,
+              "stem_wgrad_pool_bn: saved stats must be fp32 [4, 64]");
+  TORCH_CHECK(N > 0 && N * 112 < (int64_t(1) << 31), "stem_wgrad_pool_bn: bad batch");
+  const void* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    check_nhwc(*dy2, "dy2");
+    TORCH_CHECK(dy2->sizes() == dy.sizes() && dy2->device() == x.device(),
+                "stem_wgrad_pool_bn: dy2 shape");
+    d2 = dy2->data_ptr();
+  }
+  c10::DeviceGuard guard(x.device());
+  at::Tensor coef = pool_bn_coefs(dy, d2, y, vec, gamma, N * 112 * 112);
+  at::Tensor work = at::empty({(int64_t)mv_stem_wgrad_blocks((int)N) * 64 * 224},
+                              x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({64, 4, 7, 7}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  MvStemPoolBwd pb{z.data_ptr(), dy.data_ptr(), d2, idx.data_ptr<uint8_t>(),
+                   vec[2].data_ptr<float>(), vec[3].data_ptr<float>(), coef[2].data_ptr<float>(),
+                   coef[3].data_ptr<float>(), coef[4].data_ptr<float>()};
+  mv_stem_wgrad_pool_bn(x.data_ptr(), pb, dw.data_ptr(), work.data_ptr<float>(), (int)N,
+                        cur_stream(), (int)x.size(1));
+  return {dw, coef[0], coef[1]};
 }
 
 bool gemm_apply_supported(int64_t N, int64_t K) { return mv_gemm_apply_supported((int)N, (int)K); }
@@ -1765,6 +1823,8 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("maxpool_bn_bwd", &maxpool_bn_bwd,
         "{dx, dgamma, dbeta}: maxpool(3,2,1) backward fused with its producer BN+ReLU backward");
   m.def("stem_wgrad", &stem_wgrad, "ResNet stem conv weight gradient on MFMA (mv_stem.hip)");
+  m.def("stem_wgrad_pool_bn", &stem_wgrad_pool_bn,
+        "ResNet stem maxpool + BN+ReLU backward fused into the stem weight gradient -> [dw, dgamma, dbeta]");
   m.def("stem_fwd", &stem_fwd,
         "{z, [P, 2, 64] partials}: ResNet 7x7/2 stem conv on MFMA with BN statistics (mv_stem.hip)",
         py::arg("x"), py::arg("w"), py::arg("shift") = py::none(), py::arg("grid") = 0);

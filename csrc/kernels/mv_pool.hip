@@ -331,7 +331,8 @@ __global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(const __bf16* __r
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float d = __builtin_fmaf(zv[e], sc[e], bi[e]) > 0.f ? acc[i][jj][e] : 0.f;
-          acc[i][jj][e] = ka[e] * d + kb[e] * zv[e] + kc[e];
+          // explicit fma order: mv_stem.hip's fused weight gradient rebuilds these bits
+          acc[i][jj][e] = __builtin_fmaf(ka[e], d, __builtin_fmaf(kb[e], zv[e], kc[e]));
         }
       }
       store8(dx + px * g.C + c, acc[i][jj]);

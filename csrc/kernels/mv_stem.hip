@@ -252,34 +252,127 @@ __device__ __forceinline__ bf16x8 cat8(const s16x4& a, const s16x4& b) {
   return o;
 }
 
-constexpr int kWLoads = (7 * 230 + 255) / 256;   // 8-byte patch loads per thread (one row)
 
-__global__ __launch_bounds__(256) void stem_wgrad_kernel(const __bf16* __restrict__ x,
-                                                         const __bf16* __restrict__ dz,
-                                                         float* __restrict__ partial, int N,
-                                                         int cin) {
+// FUSE: dz comes from the maxpool + BN+ReLU backward (MvStemPoolBwd), built per output row
+// while it is staged (512-thread workgroups): thread t < 448 owns 8 channels of the pixel
+// pair (2b, 2b + 1) of the row, whose pooled windows are columns b, b + 1 of the 1 (even
+// row) or 2 (odd row) pooled rows covering it.  The z pair is prefetched with the next
+// row's patch; the 2 windows of a pooled row are loaded together and applied in
+// maxpool_bwd_k3s2_kernel's order (same fp32 sums, same fma epilogue -> the same dz bits).
+constexpr int kPairs = (kOW / 2) * 8;                 // (pixel pair, 8-channel group) items per row
+
+__device__ __forceinline__ void pool_bn_dz_pair(const MvStemPoolBwd& pb, const float* coef, int n,
+                                                int oh, int b, int c, const u32x4 (&zr)[2],
+                                                u32x4 (&out)[2]) {
+  constexpr int kPH = kOH / 2, kPW2 = kOW / 2;
+  float acc[2][8];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+  const int a = oh >> 1, i = oh & 1;
+  const int nda = i && a + 1 < kPH ? 2 : 1;           // uniform per row
+  const bool ok1 = b + 1 < kPW2;
+  // one pooled row at a time (both rows' windows in flight spill at 128 VGPRs)
+  for (int da = 0; da < nda; ++da) {
+    const int kh = i - 2 * da + 1;
+    u32x2 iw[2];
+    u32x4 dv[2], d2v[2];
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int col = db && !ok1 ? b : b + db;        // clamped; masked below
+      const int64_t o = (((int64_t)n * kPH + a + da) * kPW2 + col) * kCO + c;
+      iw[db] = *reinterpret_cast<const u32x2*>(pb.idx + o);
+      dv[db] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const __bf16*>(pb.dy) + o);
+      d2v[db] = pb.dy2 ? *reinterpret_cast<const u32x4*>(reinterpret_cast<const __bf16*>(pb.dy2) + o)
+                       : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      float d[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        d[2 * q] = __uint_as_float(dv[db][q] << 16);
+        d[2 * q + 1] = __uint_as_float(dv[db][q] & 0xffff0000u);
+      }
+      if (pb.dy2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          d[2 * q] += __uint_as_float(d2v[db][q] << 16);
+          d[2 * q + 1] += __uint_as_float(d2v[db][q] & 0xffff0000u);
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int kw = jj - 2 * db + 1;
+        if (kw < 0) continue;
+        const uint32_t pos = db && !ok1 ? 0xffu : (uint32_t)(kh * 3 + kw);   // 0xff: no index
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t wd = e < 4 ? iw[db][0] : iw[db][1];
+          if (((wd >> (8 * (e & 3))) & 0xffu) == pos) acc[jj][e] += d[e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[2 * q] = __uint_as_float(zr[k][q] << 16);
+      v[2 * q + 1] = __uint_as_float(zr[k][q] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float* kf = coef + c + e;      // [5][64]: scale, bias, ca, cb, cc
+      const float d = __builtin_fmaf(v[e], kf[0], kf[64]) > 0.f ? acc[k][e] : 0.f;
+      v[e] = __builtin_fmaf(kf[128], d, __builtin_fmaf(kf[192], v[e], kf[256]));
+    }
+    out[k] = u32x4{cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]), cvt_pk_bf16(v[4], v[5]),
+                   cvt_pk_bf16(v[6], v[7])};
+  }
+}
+
+// NT threads (NT / 64 waves): wave w owns output channels 16 (w % 4) .. + 15 and the
+// 14 / (NT / 256) k tiles from (w / 4) * that on — a tile's products are summed in the same
+// order whatever NT is.
+template <int NT, bool FUSE>
+__global__ __launch_bounds__(NT, FUSE ? 4 : 1) void stem_wgrad_kernel(const __bf16* __restrict__ x,
+                                                        const __bf16* __restrict__ dz,
+                                                        float* __restrict__ partial, int N,
+                                                        int cin, MvStemPoolBwd pb) {
+  static_assert(!FUSE || NT >= kPairs, "one pixel pair per thread");
+  constexpr int kTPW = 14 / (NT / 256);                // k tiles per wave
   __shared__ __attribute__((aligned(16))) __bf16 ps[7 * kPW * kC];        // 13 KB
   __shared__ __attribute__((aligned(16))) __bf16 ds[128 * 64];            // 16 KB
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int g = lane >> 4, cl = lane & 15;
+  __shared__ float coef[FUSE ? 5 * 64 : 1];
+  const int tid = threadIdx.x;
+  if constexpr (FUSE) {
+    for (int q = tid; q < 5 * 64; q += NT) {
+      const float* src[5] = {pb.scale, pb.bias, pb.ca, pb.cb, pb.cc};
+      coef[q] = src[q / 64][q % 64];
+    }
+  }
   const int64_t rows = (int64_t)N * kOH;
-  f32x4v acc[14];
+  f32x4v acc[kTPW];
 #pragma unroll
-  for (int t = 0; t < 14; ++t) acc[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < kTPW; ++t) acc[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
   // dz rows 112..127 stay zero (written once)
-  for (int q = tid; q < 16 * 8; q += 256) {
+  for (int q = tid; q < 16 * 8; q += NT) {
     const int r = 112 + q / 8, ch = q % 8;
     *reinterpret_cast<u32x4*>(ds + r * 64 + ((ch ^ dswz(r)) << 3)) = u32x4{0u, 0u, 0u, 0u};
   }
-  // next row's patch and dz in registers while the current row computes
-  constexpr int kDz = (kOW * 8 + 255) / 256;   // 16-byte dz chunks per thread
-  u32x2 pp[kWLoads];
+  // next row's patch and dz (FUSE: z pair) in registers while the current row computes
+  constexpr int kPL = (7 * 230 + NT - 1) / NT;            // 8-byte patch loads per thread
+  constexpr int kDz = FUSE ? 2 : (kOW * 8 + NT - 1) / NT;  // 16-byte dz / z chunks per thread
+  u32x2 pp[kPL];
   u32x4 pd[kDz];
-  auto gload = [&](int64_t row) {
+  auto gload = [&](int64_t row, int tid) {
     const int n = (int)(row / kOH), oh = (int)(row % kOH);
 #pragma unroll
-    for (int i = 0; i < kWLoads; ++i) {
-      const int q = tid + i * 256;
+    for (int i = 0; i < kPL; ++i) {
+      const int q = tid + i * NT;
       const int r = q / 230, pc = q % 230;
       const int ih = 2 * oh + r - 3, iw = pc - 3;
       u32x2 v = {0u, 0u};
@@ -287,52 +380,92 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(const __bf16* __restric
         v = ld_px(x, ((int64_t)n * kH + ih) * kW + iw, cin);
       pp[i] = v;
     }
-    const __bf16* dzr = dz + row * (int64_t)kOW * kCO;
+    if constexpr (FUSE) {
+      const __bf16* zr = reinterpret_cast<const __bf16*>(pb.z) + row * (int64_t)kOW * kCO;
+      const int b = tid / 8, c = (tid % 8) * 8;
 #pragma unroll
-    for (int i = 0; i < kDz; ++i) {
-      const int q = tid + i * 256;
-      pd[i] = q < kOW * 8 ? *reinterpret_cast<const u32x4*>(dzr + q * 8) : u32x4{0u, 0u, 0u, 0u};
+      for (int k = 0; k < 2; ++k)
+        pd[k] = tid < kPairs ? *reinterpret_cast<const u32x4*>(zr + (2 * b + k) * kCO + c)
+                             : u32x4{0u, 0u, 0u, 0u};
+
+    } else {
+      const __bf16* dzr = dz + row * (int64_t)kOW * kCO;
+#pragma unroll
+      for (int i = 0; i < kDz; ++i) {
+        const int q = tid + i * NT;
+        pd[i] = q < kOW * 8 ? *reinterpret_cast<const u32x4*>(dzr + q * 8) : u32x4{0u, 0u, 0u, 0u};
+      }
     }
   };
   int64_t row = blockIdx.x;
-  if (row < rows) gload(row);
+  if (row < rows) gload(row, tid);
   for (; row < rows; row += gridDim.x) {
+    // FUSE: lane-derived values recomputed per row from an opaque copy of the thread id —
+    // hoisted out of the loop, the ~60 loop-invariant LDS / global addresses spill at the
+    // 128 VGPRs of 4 waves / SIMD
+    int tid = threadIdx.x;
+    if constexpr (FUSE) asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wv = tid >> 6, g = lane >> 4, cl = lane & 15;
+    const int cw = wv & 3, t0 = (wv >> 2) * kTPW;
     __syncthreads();                        // previous row's LDS reads done
 #pragma unroll
-    for (int i = 0; i < kWLoads; ++i) {
-      const int q = tid + i * 256;
+    for (int i = 0; i < kPL; ++i) {
+      const int q = tid + i * NT;
       if (q < 7 * 230) {
         const int r = q / 230, pc = q % 230;
         *reinterpret_cast<u32x2*>(ps + (r * kPW + pc) * kC) = pp[i];
       }
     }
+    if constexpr (FUSE) {
+      if (tid < kPairs) {
+        const int oh = (int)(row % kOH);
+        const int b = tid / 8, ch = tid % 8;
+        const u32x4 zr[2] = {pd[0], pd[1]};
+        u32x4 o[2];
+        // the pooled windows are loaded here, not prefetched with the patch: holding them
+        // through the MFMA phase needs 2 waves / SIMD (3.66 vs 2.90 ms/step at bs 2048)
+        pool_bn_dz_pair(pb, coef, (int)(row / kOH), oh, b, ch * 8, zr, o);
 #pragma unroll
-    for (int i = 0; i < kDz; ++i) {
-      const int q = tid + i * 256;
-      if (q < kOW * 8) {
-        const int r = q / 8, ch = q % 8;
-        *reinterpret_cast<u32x4*>(ds + r * 64 + ((ch ^ dswz(r)) << 3)) = pd[i];
+        for (int k = 0; k < 2; ++k) {
+          const int r = 2 * b + k;
+          *reinterpret_cast<u32x4*>(ds + r * 64 + ((ch ^ dswz(r)) << 3)) = o[k];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kDz; ++i) {
+        const int q = tid + i * NT;
+        if (q < kOW * 8) {
+          const int r = q / 8, ch = q % 8;
+          *reinterpret_cast<u32x4*>(ds + r * 64 + ((ch ^ dswz(r)) << 3)) = pd[i];
+        }
       }
     }
     __syncthreads();
-    if (row + gridDim.x < rows) gload(row + gridDim.x);
+    if (row + gridDim.x < rows) gload(row + gridDim.x, tid);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int p0 = ks * 32 + 8 * g;
-      const bf16x8 af = cat8(dz_tr4(ds, p0, 16 * wv, cl), dz_tr4(ds, p0 + 4, 16 * wv, cl));
+      const bf16x8 af = cat8(dz_tr4(ds, p0, 16 * cw, cl), dz_tr4(ds, p0 + 4, 16 * cw, cl));
 #pragma unroll
-      for (int t = 0; t < 14; ++t) {
-        const int r = t >> 1, s0 = 4 * (t & 1);
+      for (int tt = 0; tt < kTPW; ++tt) {
+        const int t = t0 + tt, r = t >> 1, s0 = 4 * (t & 1);
         const bf16x8 bf = cat8(px_tr4(ps, p0, r, s0, cl), px_tr4(ps, p0 + 4, r, s0, cl));
-        acc[t] = mfma(af, bf, acc[t]);
+        acc[tt] = mfma(af, bf, acc[tt]);
       }
+      // FUSE (4 waves / SIMD): keep the fragment reads of one k step together (hoisting
+      // all 28 spills at 128 VGPRs)
+      if constexpr (FUSE) __builtin_amdgcn_sched_barrier(0);
     }
   }
-  float* pb = partial + (int64_t)blockIdx.x * kCO * 224;
+  const int lane = tid & 63, wv = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int cw = wv & 3, t0 = (wv >> 2) * kTPW;
+  float* pout = partial + (int64_t)blockIdx.x * kCO * 224;
 #pragma unroll
-  for (int t = 0; t < 14; ++t)
+  for (int tt = 0; tt < kTPW; ++tt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) pb[(16 * wv + 4 * g + r) * 224 + t * 16 + cl] = acc[t][r];
+    for (int r = 0; r < 4; ++r)
+      pout[(16 * cw + 4 * g + r) * 224 + (t0 + tt) * 16 + cl] = acc[tt][r];
 }
 
 // dw[o][r][s][c] (OHWC, s < 7) = sum_g partial[g][o][r * 32 + s * 4 + c], fixed order
@@ -374,8 +507,17 @@ int mv_stem_wgrad_blocks(int N) {
 void mv_stem_wgrad(const void* x, const void* dz, void* dw, float* work, int N, hipStream_t st,
                    int cin) {
   const int G = mv_stem_wgrad_blocks(N);
-  hipLaunchKernelGGL(mv::stem::stem_wgrad_kernel, dim3(G), dim3(256), 0, st, (const __bf16*)x,
-                     (const __bf16*)dz, work, N, cin);
+  hipLaunchKernelGGL((mv::stem::stem_wgrad_kernel<256, false>), dim3(G), dim3(256), 0, st,
+                     (const __bf16*)x, (const __bf16*)dz, work, N, cin, MvStemPoolBwd{});
+  hipLaunchKernelGGL(mv::stem::stem_wgrad_reduce_kernel, dim3((64 * 196 + 255) / 256), dim3(256), 0,
+                     st, work, G, (__bf16*)dw);
+}
+
+void mv_stem_wgrad_pool_bn(const void* x, const MvStemPoolBwd& pb, void* dw, float* work, int N,
+                           hipStream_t st, int cin) {
+  const int G = mv_stem_wgrad_blocks(N);
+  hipLaunchKernelGGL((mv::stem::stem_wgrad_kernel<512, true>), dim3(G), dim3(512), 0, st,
+                     (const __bf16*)x, (const __bf16*)nullptr, work, N, cin, pb);
   hipLaunchKernelGGL(mv::stem::stem_wgrad_reduce_kernel, dim3((64 * 196 + 255) / 256), dim3(256), 0,
                      st, work, G, (__bf16*)dw);
 }

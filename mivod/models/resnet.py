@@ -74,21 +74,32 @@ class StemConv(nn.Conv2d):
     faster fwd+wgrad (scripts/micro_stem.py).  The zero channel contributes
     nothing, and its weight gradient is sliced away, so the math is unchanged."""
 
+    def stem_kernel_ok(self, x) -> bool:
+        """mivod's stem kernels apply: not MIVOD_STEM_KERNEL=0, a 224x224 bf16 channels_last
+        GPU image, the ResNet stem geometry."""
+        return not (os.environ.get("MIVOD_STEM_KERNEL", "1") == "0" or not x.is_cuda
+                    or x.dtype != torch.bfloat16 or x.dim() != 4
+                    or tuple(x.shape[1:]) != (3, 224, 224)
+                    or not x.is_contiguous(memory_format=torch.channels_last)
+                    or self.weight.dtype != torch.bfloat16
+                    or tuple(self.weight.shape) != (64, 3, 7, 7)
+                    or tuple(self.stride) != (2, 2) or tuple(self.padding) != (3, 3)
+                    or self.bias is not None or self.groups != 1
+                    or tuple(self.dilation) != (1, 1))
+
+    def kernel_operands(self, x):
+        """(image, 4-channel OHWC filter) as the stem kernels take them: the kernels read the
+        3-channel image directly (MIVOD_STEM_PAD_INPUT=1: pad it first)."""
+        w = F.pad(self.weight, (0, 0, 0, 0, 0, 1)).contiguous(memory_format=torch.channels_last)
+        xin = pad_channels(x, 4) if os.environ.get("MIVOD_STEM_PAD_INPUT", "0") == "1" else x
+        return xin, w
+
     def forward_stats(self, x, shift):
         """(conv(x), [P, 2, 64] BN statistics partials around ``shift``) on mivod's stem
-        kernel, or None when it does not apply (MIVOD_STEM_KERNEL=0, not a 224x224 bf16
-        channels_last GPU image, not the ResNet stem geometry)."""
-        if (os.environ.get("MIVOD_STEM_KERNEL", "1") == "0" or not x.is_cuda
-                or x.dtype != torch.bfloat16 or x.dim() != 4 or tuple(x.shape[1:]) != (3, 224, 224)
-                or not x.is_contiguous(memory_format=torch.channels_last)
-                or self.weight.dtype != torch.bfloat16 or tuple(self.weight.shape) != (64, 3, 7, 7)
-                or tuple(self.stride) != (2, 2) or tuple(self.padding) != (3, 3)
-                or self.bias is not None or self.groups != 1 or tuple(self.dilation) != (1, 1)):
+        kernel, or None when it does not apply (see stem_kernel_ok)."""
+        if not self.stem_kernel_ok(x):
             return None
-        w = F.pad(self.weight, (0, 0, 0, 0, 0, 1)).contiguous(memory_format=torch.channels_last)
-        # the kernels read the 3-channel image directly (MIVOD_STEM_PAD_INPUT=1: pad it first)
-        xin = pad_channels(x, 4) if os.environ.get("MIVOD_STEM_PAD_INPUT", "0") == "1" else x
-        return _StemConvStats.apply(xin, w, shift)
+        return _StemConvStats.apply(*self.kernel_operands(x), shift)
 
     def forward(self, x):
         cp = int(os.environ.get("MIVOD_STEM_CHANNELS", "4"))
@@ -99,6 +110,60 @@ class StemConv(nn.Conv2d):
                 memory_format=torch.channels_last)
             return F.conv2d(pad_channels(x, cp), w, None, self.stride, self.padding)
         return super().forward(x)
+
+
+class _StemBNReluMaxPool(torch.autograd.Function):
+    """maxpool(relu(bn(stem_conv(x)))) with ONE backward pass over the stem rows: the
+    pooled-level BN reduce (mv_pool.hip), then the stem weight-gradient kernel rebuilds each
+    row's dz from the conv output and the pooled gradients while staging it
+    (mv_stem.hip, MvStemPoolBwd) — the full-resolution dz (3.3 GB at bs 2048) is never
+    written or read back.  Forward = _StemConvStats + ops.bn._BNReluMaxPool's kernels.
+    The image gets no gradient (as in _StemConvStats)."""
+
+    @staticmethod
+    def forward(ctx, x4, w4, weight, bias, running_mean, running_var, momentum, eps, slot):
+        from ..ops import kernels as K
+        nat = K.native()
+        z, part = nat.stem_fwd(x4, w4, running_mean)
+        vec = nat.bn_finalize(part, weight, bias, running_mean, running_var, momentum, eps,
+                              z.numel() // z.shape[1])
+        y, idx = nat.maxpool_fwd(z, vec[2], vec[3], True, 3, 2, 1)
+        ctx.save_for_backward(x4, z, vec, weight, idx, y)
+        ctx.slot = slot
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import kernels as K
+        x4, z, vec, weight, idx, y = ctx.saved_tensors
+        dw, dg, db = K.native().stem_wgrad_pool_bn(
+            x4, dy.contiguous(memory_format=torch.channels_last), ctx.slot.take(), idx, y, z,
+            vec, weight)
+        return (None, dw if ctx.needs_input_grad[1] else None,
+                dg if ctx.needs_input_grad[2] else None,
+                db if ctx.needs_input_grad[3] else None, None, None, None, None, None)
+
+
+def stem_bn_relu_maxpool(conv: "StemConv", bn: BatchNorm2d, pool: nn.MaxPool2d, x):
+    """``pool(relu(bn(conv(x))))`` on _StemBNReluMaxPool, or None when it does not apply
+    (MIVOD_STEM_POOL_FUSE=0, not training with running statistics, another pool window,
+    an image that needs a gradient, the stem kernels off)."""
+    if (os.environ.get("MIVOD_STEM_POOL_FUSE", "1") == "0" or not _bn._POOL_BN_BWD
+            or os.environ.get("MIVOD_FUSED_BN", "1") == "0"
+            or not (bn.training and bn.track_running_stats) or bn.weight is None
+            or bn.bias is None or bn.weight.dtype != torch.float32
+            or _bn._pool_args(pool) != (3, 2, 1) or x.requires_grad
+            or not conv.stem_kernel_ok(x)):
+        return None
+    bn._mv_steps += 1
+    momentum = bn.momentum
+    if momentum is None:
+        momentum = 1.0 / float(bn._mv_steps + int(bn.num_batches_tracked.item()))
+    slot = _bn.GradSlot()
+    y = _StemBNReluMaxPool.apply(*conv.kernel_operands(x), bn.weight, bn.bias, bn.running_mean,
+                                 bn.running_var, float(momentum), float(bn.eps), slot)
+    y._mv_slot = slot
+    return y
 
 
 class Bottleneck(nn.Module):
@@ -225,6 +290,10 @@ class ResNet(nn.Module):
 
     def _forward(self, x):
         r = None
+        y = stem_bn_relu_maxpool(self.conv1, self.bn1, self.maxpool, x)
+        if y is not None:
+            x = self.layer4(self.layer3(self.layer2(self.layer1(y))))
+            return self.fc(global_avg_pool(x))
         if self.bn1.training and self.bn1.track_running_stats:
             r = self.conv1.forward_stats(x, self.bn1.running_mean)
         if r is not None:       # stem conv with the BN statistics in its epilogue
