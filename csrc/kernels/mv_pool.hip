@@ -365,6 +365,8 @@ __global__ __launch_bounds__(256) void pool_bn_reduce_kernel(
       isc[e] = scv != 0.f ? 1.f / scv : 0.f;
       bi[e] = bias[c + e];
     }
+    // 4 rows' loads in flight per lane (one row per iteration ran at ~2.9 TB/s)
+#pragma unroll 4
     for (int64_t r = (int64_t)blockIdx.x * rpi + tr; r < M; r += (int64_t)gridDim.x * rpi) {
       float gv[8], yv[8];
       load8_nt(dy + r * C + c, gv);
