@@ -1095,6 +1095,29 @@ static void fold_check_f32(const at::Tensor& t, int64_t n, const at::Device& d, 
 // reduce partials part [P, 2, cout], W [cout, cin] (bf16), g = dz^T x [cout, cin] (fp32),
 // the BN's saved vec [4, cout] and gamma; xsum from colsum partials [P2, cin] (or zeros
 // when colsum is None — the caller supplies it)
+// [1, 2, cout] BN statistics partials of z = x W^T around shift from the Gram matrix
+// gram = x^T x ([cin, cin] fp32) and xsum = colsum(x) [cin] (mv_fold.hip gram_stats_kernel)
+at::Tensor gram_stats(at::Tensor w, at::Tensor gram, at::Tensor xsum,
+                      c10::optional<at::Tensor> shift, int64_t m) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() &&
+                  w.dim() == 2, "gram_stats: W must be contiguous bf16 [cout, cin]");
+  const int64_t cout = w.size(0), cin = w.size(1);
+  TORCH_CHECK(gram.device() == w.device() && gram.scalar_type() == at::kFloat &&
+                  gram.is_contiguous() && gram.numel() == cin * cin,
+              "gram_stats: gram must be contiguous fp32 [cin, cin]");
+  TORCH_CHECK(xsum.device() == w.device() && xsum.scalar_type() == at::kFloat &&
+                  xsum.is_contiguous() && xsum.numel() == cin,
+              "gram_stats: xsum must be contiguous fp32 [cin]");
+  TORCH_CHECK(m > 0, "gram_stats: m must be positive");
+  const float* sh = opt_f32(shift, cout, "shift");
+  c10::DeviceGuard guard(w.device());
+  at::Tensor part = at::empty({1, 2, cout}, gram.options());
+  TORCH_CHECK(mv_gram_stats(w.data_ptr(), gram.data_ptr<float>(), xsum.data_ptr<float>(), sh, m,
+                            (int)cout, (int)cin, part.data_ptr<float>(), cur_stream()),
+              "gram_stats: needs cout % 16 == 0 and cin <= 1024");
+  return part;
+}
+
 std::vector<at::Tensor> fold_coeffs(at::Tensor part, at::Tensor w, at::Tensor g, at::Tensor vec,
                                     c10::optional<at::Tensor> gamma, int64_t M,
                                     c10::optional<at::Tensor> colsum) {
@@ -1822,6 +1845,10 @@ PYBIND11_MODULE(_mvk, m) {
   m.def("gemm_apply_supported", &gemm_apply_supported, "gemm_nt_apply handles (N, K)");
   m.def("maxpool_bn_bwd", &maxpool_bn_bwd,
         "{dx, dgamma, dbeta}: maxpool(3,2,1) backward fused with its producer BN+ReLU backward");
+  m.def("gram_stats", &gram_stats,
+        "[1, 2, cout] BN statistics partials of x W^T from the Gram matrix x^T x and colsum(x)",
+        py::arg("w"), py::arg("gram"), py::arg("xsum"), py::arg("shift") = py::none(),
+        py::arg("m") = 1);
   m.def("stem_wgrad", &stem_wgrad, "ResNet stem conv weight gradient on MFMA (mv_stem.hip)");
   m.def("stem_wgrad_pool_bn", &stem_wgrad_pool_bn,
         "ResNet stem maxpool + BN+ReLU backward fused into the stem weight gradient -> [dw, dgamma, dbeta]");

@@ -12,3 +12,8 @@ void mv_fold_coeffs(const float* part, int P, const void* w, const float* g, con
 void mv_fold_products(const void* w, const float* g, const float* gram, const float* co,
                       const float* xsum, int cout, int cin, void* dw, void* bcat, float* badd,
                       hipStream_t st);
+// part [2][cout] = (sum (z - shift), sum (z - shift)^2) of z = x W^T from G = x^T x
+// [cin][cin] fp32 and xsum [cin] = colsum(x); W [cout][cin] bf16, shift may be null.
+// false (nothing launched): cout % 16 != 0 or cin > 1024
+bool mv_gram_stats(const void* w, const float* gram, const float* xsum, const float* shift,
+                   int64_t m, int cout, int cin, float* part, hipStream_t st);

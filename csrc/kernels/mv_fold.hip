@@ -193,8 +193,89 @@ __global__ __launch_bounds__(kThreads) void fold_products_kernel(
   }
 }
 
+// BN statistics partials of z = x W^T from the Gram matrix G = x^T x (ops.bn._gram_stats):
+//   part[0][c] = sum_k W[c][k] xsum[k] - m shift[c]                        = sum (z - shift)
+//   part[1][c] = sum_k W[c][k] (G W^T)[k][c] - 2 shift[c] u[c] + m shift[c]^2  = sum (z - shift)^2
+// One workgroup per 16 output channels: W's rows in LDS (fp32), thread t owns Gram rows
+// k = t, t + 256, .. and reads G[j][k] (= G[k][j]: coalesced across threads) for all j,
+// then a fixed-order block reduction per channel.
+constexpr int kGsCh = 16;
+
+__global__ __launch_bounds__(kThreads) void gram_stats_kernel(
+    const __bf16* __restrict__ w, const float* __restrict__ gram, const float* __restrict__ xsum,
+    const float* __restrict__ shift, int64_t m, int cout, int cin, float* __restrict__ part) {
+  extern __shared__ float gs_smem[];
+  float* wl = gs_smem;                              // [kGsCh][cin]
+  float* red = gs_smem + kGsCh * cin;               // [2][kGsCh][kThreads / 64]
+  const int c0 = blockIdx.x * kGsCh, tid = threadIdx.x;
+  for (int q = tid; q < kGsCh * cin; q += kThreads) {
+    const int r = q / cin, k = q - r * cin;
+    wl[q] = (float)w[(int64_t)(c0 + r) * cin + k];
+  }
+  __syncthreads();
+  float qs[kGsCh], us[kGsCh];
+#pragma unroll
+  for (int r = 0; r < kGsCh; ++r) { qs[r] = 0.f; us[r] = 0.f; }
+  for (int k = tid; k < cin; k += kThreads) {
+    float t[kGsCh];
+#pragma unroll
+    for (int r = 0; r < kGsCh; ++r) t[r] = 0.f;
+    // 8 Gram loads in flight per thread (a serial chain of L2 round trips otherwise)
+#pragma unroll 8
+    for (int j = 0; j < cin; ++j) {
+      const float g = gram[(int64_t)j * cin + k];
+#pragma unroll
+      for (int r = 0; r < kGsCh; ++r) t[r] = __builtin_fmaf(g, wl[r * cin + j], t[r]);
+    }
+    const float xs = xsum[k];
+#pragma unroll
+    for (int r = 0; r < kGsCh; ++r) {
+      qs[r] = __builtin_fmaf(wl[r * cin + k], t[r], qs[r]);
+      us[r] = __builtin_fmaf(wl[r * cin + k], xs, us[r]);
+    }
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int r = 0; r < kGsCh; ++r) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      qs[r] += __shfl_xor(qs[r], o, 64);
+      us[r] += __shfl_xor(us[r], o, 64);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < kGsCh; ++r) {
+      red[(0 * kGsCh + r) * (kThreads / 64) + wv] = qs[r];
+      red[(1 * kGsCh + r) * (kThreads / 64) + wv] = us[r];
+    }
+  }
+  __syncthreads();
+  if (tid < kGsCh) {
+    float q = 0.f, u = 0.f;
+    for (int i = 0; i < kThreads / 64; ++i) {
+      q += red[(0 * kGsCh + tid) * (kThreads / 64) + i];
+      u += red[(1 * kGsCh + tid) * (kThreads / 64) + i];
+    }
+    const int c = c0 + tid;
+    const float sh = shift ? shift[c] : 0.f, mf = (float)m;
+    part[c] = u - mf * sh;
+    part[cout + c] = q - 2.f * sh * u + mf * sh * sh;
+  }
+}
+
 }  // namespace fold
 }  // namespace mv
+
+bool mv_gram_stats(const void* w, const float* gram, const float* xsum, const float* shift,
+                   int64_t m, int cout, int cin, float* part, hipStream_t st) {
+  using namespace mv::fold;
+  if (cout % kGsCh || cin < 1 || cin > 1024) return false;
+  const size_t lds = (size_t)(kGsCh * cin + 2 * kGsCh * (kThreads / 64)) * sizeof(float);
+  hipLaunchKernelGGL(gram_stats_kernel, dim3(cout / kGsCh), dim3(kThreads), lds, st,
+                     (const __bf16*)w, gram, xsum, shift, m, cout, cin, part);
+  return true;
+}
 
 void mv_fold_coeffs(const float* part, int P, const void* w, const float* g, const float* vec,
                     const float* gamma, int64_t M, int cout, int cin, const float* colsum, int P2,

@@ -42,6 +42,9 @@ _SHORTCUT_FOLD = os.environ.get("MIVOD_BN_SHORTCUT_FOLD", "1") != "0"
 # MIVOD_BN_COLSUM=0: the fold's colsum(x) term reads x in a statistics pass instead of
 # taking BN2's apply-pass column sums
 _COLSUM = os.environ.get("MIVOD_BN_COLSUM", "1") != "0"
+# MIVOD_BN_STATS_GRAM=0: the recomputed expansion conv's BN statistics come from a
+# statistics-only GEMM pass over z = x W^T instead of x's Gram matrix (_gram_stats)
+_GRAM_STATS = os.environ.get("MIVOD_BN_STATS_GRAM", "1") != "0"
 # MIVOD_BN_SHORTCUT_DUAL=0: a stride-1 shortcut conv's output is written by its statistics
 # GEMM and read back as the residual, instead of being recomputed inside conv3's apply GEMM
 _SHORTCUT_DUAL = os.environ.get("MIVOD_BN_SHORTCUT_DUAL", "1") != "0"
@@ -53,6 +56,18 @@ _FOLD_MATH = os.environ.get("MIVOD_BN_FOLD_MATH", "1") != "0"
 _POOL_BN_BWD = os.environ.get("MIVOD_POOL_BN_BWD", "1") != "0"
 # MIVOD_BN_DUAL_WGRAD=0: the fold's dz^T x and Gram x^T x as two wgrad1x1 launches
 _DUAL_WGRAD = os.environ.get("MIVOD_BN_DUAL_WGRAD", "1") != "0"
+
+
+def _gram_stats(nat, x, w2, colsum, shift, m):
+    """[1, 2, cout] statistics partials of z = x W^T around ``shift`` without computing z:
+    sum z = W colsum(x) and sum z^2 = rowsum((W G) * W) with G = x^T x (mivod's wgrad1x1
+    kernel, fp32) — one pass over x at 2 m cin^2 flops instead of the GEMM's 2 m cin cout,
+    and colsum(x) comes for free from the producing BN's apply (``colsum`` [P, cin]); the
+    [cout]-sized remainder is one kernel (mv_fold.hip gram_stats_kernel).
+    Sums of the fp32 products: z itself is later rounded to bf16 (a ~2^-9 relative
+    difference per element that the statistics average out)."""
+    g = nat.wgrad1x1(x, x, 1, True)
+    return nat.gram_stats(w2.contiguous(), g, colsum.sum(0), shift, m)
 
 
 def _fold_math(nat, wb, g, gram, vec, gamma, m, part, sdz, colsum, xs_fn, need_w):
@@ -602,9 +617,14 @@ class _Conv1x1BNFold(torch.autograd.Function):
             m = n * h * wd
             x2 = x.permute(0, 2, 3, 1).reshape(m, cin)
             w2 = w.permute(0, 2, 3, 1).reshape(cout, cin)
-            part = torch.empty(nat.gemm_partials(m, cout, cin), 2, cout, dtype=torch.float32,
-                               device=x.device)
-            nat.gemm_nt(x2, w2, None, running_mean, part)
+            xcs = getattr(getattr(x, "_mv_slot", None), "colsum", None)
+            if (_GRAM_STATS and xcs is not None and cin % 64 == 0 and cin <= 1024
+                    and cout % 16 == 0):
+                part = _gram_stats(nat, x, w2, xcs, running_mean, m)
+            else:
+                part = torch.empty(nat.gemm_partials(m, cout, cin), 2, cout,
+                                   dtype=torch.float32, device=x.device)
+                nat.gemm_nt(x2, w2, None, running_mean, part)
             vec = nat.bn_finalize(part, weight, bias, running_mean, running_var, momentum, eps, m)
             if dual is not None:
                 yf, keep = nat.gemm_nt_apply_dual(x2, w2, dual[0], dual[1], vec[2], vec[3],
