@@ -205,12 +205,12 @@ __global__ __launch_bounds__(kThreads) void gram_stats_kernel(
     const __bf16* __restrict__ w, const float* __restrict__ gram, const float* __restrict__ xsum,
     const float* __restrict__ shift, int64_t m, int cout, int cin, float* __restrict__ part) {
   extern __shared__ float gs_smem[];
-  float* wl = gs_smem;                              // [kGsCh][cin]
+  float* wl = gs_smem;                              // [cin][kGsCh]: W^T rows, 4 x 16-byte reads
   float* red = gs_smem + kGsCh * cin;               // [2][kGsCh][kThreads / 64]
   const int c0 = blockIdx.x * kGsCh, tid = threadIdx.x;
   for (int q = tid; q < kGsCh * cin; q += kThreads) {
     const int r = q / cin, k = q - r * cin;
-    wl[q] = (float)w[(int64_t)(c0 + r) * cin + k];
+    wl[k * kGsCh + r] = (float)w[(int64_t)(c0 + r) * cin + k];
   }
   __syncthreads();
   float qs[kGsCh], us[kGsCh];
@@ -224,14 +224,19 @@ __global__ __launch_bounds__(kThreads) void gram_stats_kernel(
 #pragma unroll 8
     for (int j = 0; j < cin; ++j) {
       const float g = gram[(int64_t)j * cin + k];
+      const f32x4* wj = reinterpret_cast<const f32x4*>(wl + j * kGsCh);
 #pragma unroll
-      for (int r = 0; r < kGsCh; ++r) t[r] = __builtin_fmaf(g, wl[r * cin + j], t[r]);
+      for (int h = 0; h < kGsCh / 4; ++h) {
+        const f32x4 wv = wj[h];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t[4 * h + e] = __builtin_fmaf(g, wv[e], t[4 * h + e]);
+      }
     }
     const float xs = xsum[k];
 #pragma unroll
     for (int r = 0; r < kGsCh; ++r) {
-      qs[r] = __builtin_fmaf(wl[r * cin + k], t[r], qs[r]);
-      us[r] = __builtin_fmaf(wl[r * cin + k], xs, us[r]);
+      qs[r] = __builtin_fmaf(wl[k * kGsCh + r], t[r], qs[r]);
+      us[r] = __builtin_fmaf(wl[k * kGsCh + r], xs, us[r]);
     }
   }
   const int lane = tid & 63, wv = tid >> 6;

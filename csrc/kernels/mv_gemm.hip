@@ -640,8 +640,9 @@ static bool stream_cfg(int K, int N, int* bn) {
 // rows per streamed tile: the K = 256 backward-reduce variant streams 32-row tiles so two
 // workgroups fit a CU (its 64 KB filter slice + 16 KB A tile) — its epilogue reads three
 // [M, N] operands, so resident waves matter more than MFMA tile depth
+// (the K = 256 apply epilogues likewise: one 96 KB workgroup per CU at 64 rows)
 template <int K, int EPI>
-constexpr int stream_bm() { return (K == 256 && EPI == 2) ? 32 : 64; }
+constexpr int stream_bm() { return (K == 256 && (EPI == 2 || EPI == 3 || EPI == 5)) ? 32 : 64; }
 
 template <int K, int BN, int EPI>
 static int64_t streams_for(int64_t M, int N) {
@@ -704,13 +705,15 @@ static void launch_apply(const __bf16* a, const __bf16* b, __bf16* y, int64_t M,
                            ntn, ntm, nullptr, nullptr, e);
       }
     } else if (e.rsc) {
+      constexpr int BMV = stream_bm<K, 5>();
       const dim3 grid((unsigned)(streams_for<K, BN, 5>(M, N) * ntn));
-      hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 5>), grid, dim3(256), 0, st, a, b, y, M, N,
-                         ntn, ntm, nullptr, nullptr, e);
+      hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 5, BMV>), grid, dim3(256), 0, st, a, b, y, M,
+                         N, ntn, (M + BMV - 1) / BMV, nullptr, nullptr, e);
     } else {
+      constexpr int BMV = stream_bm<K, 3>();
       const dim3 grid((unsigned)(streams_for<K, BN, 3>(M, N) * ntn));
-      hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 3>), grid, dim3(256), 0, st, a, b, y, M, N,
-                         ntn, ntm, nullptr, nullptr, e);
+      hipLaunchKernelGGL((gemm_stream_kernel<K, BN, 3, BMV>), grid, dim3(256), 0, st, a, b, y, M,
+                         N, ntn, (M + BMV - 1) / BMV, nullptr, nullptr, e);
     }
   }
 }

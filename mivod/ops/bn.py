@@ -22,11 +22,12 @@ from . import kernels as K
 _BN_MASK = os.environ.get("MIVOD_BN_MASK", "1") != "0"
 # MIVOD_BN_RECOMPUTE=0: the BN3 fold materialises z and runs the separate apply pass (A/B)
 _RECOMPUTE = os.environ.get("MIVOD_BN_RECOMPUTE", "1") != "0"
-# ... for K = Cin <= MIVOD_BN_RECOMPUTE_MAXK (default 128): at K = 256 (ResNet-50 layer3) the
-# second GEMM's compute (~0.4 ms at bs 2048) is about what the z write + read saves (bench A/B
-# 128 vs 256: 15,294 / 15,330 vs 15,304 / 15,282 img/s, level); blocks with a projection
-# shortcut keep it (its BN is applied in that epilogue)
-_RECOMPUTE_MAXK = int(os.environ.get("MIVOD_BN_RECOMPUTE_MAXK", "128"))
+# ... for K = Cin <= MIVOD_BN_RECOMPUTE_MAXK (default 256; blocks with a projection shortcut
+# always, their BN is applied in that epilogue).  With a statistics-only GEMM pass, K = 256
+# (ResNet-50 layer3) was level (round 2: 15,294 / 15,330 vs 15,304 / 15,282 img/s at 128 vs
+# 256); with the Gram statistics (_gram_stats) and 32-row apply tiles it wins (round 3 A/B:
+# 17,441 vs 17,283 img/s)
+_RECOMPUTE_MAXK = int(os.environ.get("MIVOD_BN_RECOMPUTE_MAXK", "256"))
 # the 256 x 256 GEMM (mv_gemm256.hip) for the strided shortcut forward
 _GEMM256 = os.environ.get("MIVOD_GEMM256", "1") != "0"
 # MIVOD_BN_FOLD_DX=0: the fold's data gradient runs as two hipBLASLt GEMMs and BN2 runs its
