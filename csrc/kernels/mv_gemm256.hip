@@ -601,6 +601,10 @@ struct WArgs {
   // column tile is 256 channels of ONE tap (Cx % 256 == 0) — and X rows are gathered:
   // output pixel (n, ho, wo) reads input pixel (n, ho ds - 1 + r, wo ds - 1 + s)
   int Cx, H, W, Ho, Wo, ds;
+  // magic multipliers ceil(2^32 / d) for d = Ho Wo and Wo (0: divide): q = umulhi(n, mg) is
+  // exact for n d < 2^32 (the host checks M Ho Wo < 2^32) — the two per-row divisions were
+  // ~2 VALU instructions per MFMA
+  uint32_t mg_hw, mg_wo;
 };
 
 __device__ __forceinline__ int wf(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
@@ -676,9 +680,10 @@ __global__ __launch_bounds__(NT, 1) void wgrad256_kernel(WArgs p) {
           xpix[i] = -1;
           if (row < me) {            // (M < 2^31: 32-bit unsigned divisions)
             const uint32_t r32 = (uint32_t)row, hw = (uint32_t)(p.Ho * p.Wo);
-            const uint32_t n = r32 / hw;
+            const uint32_t n = p.mg_hw ? __umulhi(r32, p.mg_hw) : r32 / hw;
             const uint32_t rem = r32 - n * hw;
-            const uint32_t ho = rem / (uint32_t)p.Wo, wo = rem - ho * (uint32_t)p.Wo;
+            const uint32_t ho = p.mg_wo ? __umulhi(rem, p.mg_wo) : rem / (uint32_t)p.Wo;
+            const uint32_t wo = rem - ho * (uint32_t)p.Wo;
             const int hi = (int)ho * p.ds - 1 + tr, wi = (int)wo * p.ds - 1 + ts;
             if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
               xpix[i] = ((int64_t)n * p.H + hi) * p.W + wi;
@@ -1100,6 +1105,14 @@ bool mv_wgrad256_3x3(const void* X, const void* DY, float* partial, int N, int H
   a.ds = stride;
   a.ntc = a.C / 256;
   a.ntiles = (a.C / 256) * (K / 256);
+  {
+    const uint64_t hw = (uint64_t)a.Ho * a.Wo;
+    auto magic = [](uint64_t d) { return (uint32_t)(((uint64_t(1) << 32) + d - 1) / d); };
+    if (hw >= 2 && a.Wo >= 2 && (uint64_t)a.M * hw < (uint64_t(1) << 32)) {
+      a.mg_hw = magic(hw);
+      a.mg_wo = magic((uint64_t)a.Wo);
+    }
+  }
   w256_split(a.M, a.C, K, &a.ms, &a.per);
   hipLaunchKernelGGL(wgrad256_kernel<9>, dim3((unsigned)(a.ntiles * a.ms)), dim3(NT), 0, st, a);
   return true;
