@@ -93,17 +93,18 @@ __device__ __forceinline__ void row_info(const Geo& g, const __bf16* X, int64_t 
     ri.addr[i] = 0;
     if (DG && m < g.M) {
       // class row (n, ci, cj) reads dy (n, ci + di, cj + dj): bit 2 di + dj when inside dy
-      const int hw = g.Ho * g.Wo;
-      const int rem = (int)(m % hw);
-      const int ci = rem / g.Wo, cj = rem - ci * g.Wo;
+      // (rows < 2^31: 32-bit unsigned divisions, several times cheaper than 64-bit ones)
+      const uint32_t hw = (uint32_t)(g.Ho * g.Wo);
+      const int rem = (int)((uint32_t)m % hw);
+      const int ci = (int)((uint32_t)rem / (uint32_t)g.Wo), cj = rem - ci * g.Wo;
       const bool r1 = ci + 1 < g.Ho, c1 = cj + 1 < g.Wo;
       ri.valid[i] = 1u | (c1 ? 2u : 0u) | (r1 ? 4u : 0u) | (r1 && c1 ? 8u : 0u);
       ri.addr[i] = (uint64_t)(X + (m * g.C + sc * 8));
     } else if (m < g.M) {
-      const int64_t hw = (int64_t)g.Ho * g.Wo;
-      const int n = (int)(m / hw);
-      const int rem = (int)(m - (int64_t)n * hw);
-      const int ho = rem / g.Wo, wo = rem - ho * g.Wo;
+      const uint32_t hw = (uint32_t)(g.Ho * g.Wo), m32 = (uint32_t)m;
+      const int n = (int)(m32 / hw);
+      const int rem = (int)(m32 - (uint32_t)n * hw);
+      const int ho = (int)((uint32_t)rem / (uint32_t)g.Wo), wo = rem - ho * g.Wo;
       const int pad = g.ks >> 1;
       const int hi0 = ho * g.st - pad, wi0 = wo * g.st - pad;
       uint32_t v = 0;
@@ -446,6 +447,8 @@ bool mv_conv_nhwc(const void* x, const void* w, void* y, int N, int H, int W, in
   using namespace mv::conv;
   if (C % 64 != 0 || K % 64 != 0 || (stride != 1 && stride != 2) || (ks != 1 && ks != 3))
     return false;
+  // row_info's 32-bit pixel divisions need N * H * W < 2^31
+  if ((int64_t)N * H * W >= (int64_t(1) << 31)) return false;
   const bool bna = in_scale != nullptr;
   // 64 -> 64 channel 3x3 stride 1 (ResNet-50 layer1): the row-patch kernel (mv_conv64.hip)
   static const bool c64 = [] {
@@ -588,7 +591,8 @@ void mv_transpose_filters(const void* table, int n, int64_t blocks, hipStream_t 
 bool mv_conv3x3_s2_dgrad_supported(int Nb, int H, int W, int C, int K) {
   if (mv_dgrad256_s2_supported(Nb, H, W, C, K)) return true;
   return Nb > 0 && H >= 2 && W >= 2 && !(H & 1) && !(W & 1) && C % 64 == 0 && K % 64 == 0 &&
-         C > 0 && K > 0 && (int64_t)Nb * H * W * std::max(C, K) < (int64_t(1) << 40);
+         C > 0 && K > 0 && (int64_t)Nb * H * W * std::max(C, K) < (int64_t(1) << 40) &&
+         (int64_t)Nb * H * W < (int64_t(1) << 31);
 }
 
 bool mv_conv3x3_s2_dgrad(const void* dy, const void* wt, void* dx, int Nb, int H, int W, int C,

@@ -181,18 +181,18 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
         int64_t row = mt * BMv + (r >> 6) * (MT * 16) + h * 64 +
                       ((h == 1 && rr >= 16 * MH1) ? rr - 16 * MH1 : rr);
         row = row < p.M ? row : p.M - 1;           // rows past M: a valid row, never stored
-        if constexpr (AMODE == 1) {
-          const int64_t hw = (int64_t)p.Ho * p.Wo;
-          const int64_t n = row / hw;
-          const int rem = (int)(row - n * hw);
-          const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+        if constexpr (AMODE == 1) {          // rows < 2^31: 32-bit unsigned divisions
+          const uint32_t hw = (uint32_t)(p.Ho * p.Wo), r32 = (uint32_t)row;
+          const int64_t n = r32 / hw;
+          const int rem = (int)(r32 - (uint32_t)n * hw);
+          const int ho = (int)((uint32_t)rem / (uint32_t)p.Wo), wo = rem - ho * p.Wo;
           row = (n * p.H + (int64_t)ho * p.ds) * p.W + (int64_t)wo * p.ds;
         }
-        if constexpr (AMODE == 3) {
-          const int64_t hw = (int64_t)p.Ho * p.Wo;
-          const int64_t n = row / hw;
-          const int rem = (int)(row - n * hw);
-          const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+        if constexpr (AMODE == 3) {          // rows < 2^31: 32-bit unsigned divisions
+          const uint32_t hw = (uint32_t)(p.Ho * p.Wo), r32 = (uint32_t)row;
+          const int64_t n = r32 / hw;
+          const int rem = (int)(r32 - (uint32_t)n * hw);
+          const int ho = (int)((uint32_t)rem / (uint32_t)p.Wo), wo = rem - ho * p.Wo;
           const int pad = p.ks >> 1;
           const int hi0 = ho * p.ds - pad, wi0 = wo * p.ds - pad;
           uint32_t v = 0;
@@ -212,9 +212,9 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
         if constexpr (AMODE == 4) {
           // class row (n, ci, cj) reads dy (n, ci + di, cj + dj), di, dj in {0, 1}: bit
           // 2 di + dj set when that pixel is inside dy
-          const int hw = p.Ho * p.Wo;
-          const int rem = (int)(row % hw);
-          const int ci = rem / p.Wo, cj = rem - ci * p.Wo;
+          const uint32_t hw = (uint32_t)(p.Ho * p.Wo);
+          const int rem = (int)((uint32_t)row % hw);
+          const int ci = (int)((uint32_t)rem / (uint32_t)p.Wo), cj = rem - ci * p.Wo;
           const bool r1 = ci + 1 < p.Ho, c1 = cj + 1 < p.Wo;
           const uint32_t v = 1u | (c1 ? 2u : 0u) | (r1 ? 4u : 0u) | (r1 && c1 ? 8u : 0u);
           if (i == 0) avalid[h] = v;
@@ -225,10 +225,10 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
           offa[h][i] = (uint32_t)row;
           int64_t row2 = row;
           if (p.ds > 1) {          // A2 = x [*, H, W, K2] read at the output row's stride pixel
-            const int64_t hw = (int64_t)p.Ho * p.Wo;
-            const int64_t n = row / hw;
-            const int rem = (int)(row - n * hw);
-            const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+            const uint32_t hw = (uint32_t)(p.Ho * p.Wo), r32 = (uint32_t)row;
+            const int64_t n = r32 / hw;
+            const int rem = (int)(r32 - (uint32_t)n * hw);
+            const int ho = (int)((uint32_t)rem / (uint32_t)p.Wo), wo = rem - ho * p.Wo;
             row2 = (n * p.H + (int64_t)ho * p.ds) * p.W + (int64_t)wo * p.ds;
           }
           offa2[h][i] = (uint32_t)row2;
