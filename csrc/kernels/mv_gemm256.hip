@@ -168,6 +168,10 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
   const uint32_t scb = (uint32_t)(((lane & 7) ^ ((lane >> 3) & 7)) * 16);   // = sc * 16 bytes
   const int KT = p.K / BK, KT1 = AMODE == 2 ? p.K1 / BK : KT;
   const int csteps = (AMODE == 3 || AMODE == 4) ? p.Cin / BK : 1;
+  // K tile -> (tap, channel step) by shift when csteps is a power of two (Cin = 256 / 512 /
+  // ..: always on ResNet shapes) — two scalar divisions per issued K tile otherwise
+  const bool cpow2 = (csteps & (csteps - 1)) == 0;
+  const int cshift = __builtin_ctz((unsigned)csteps);
   auto set_src = [&](int64_t tl) {
     const int64_t mt = tl / p.ntn;
     const int nt = (int)(tl - mt * p.ntn);
@@ -245,14 +249,15 @@ __global__ __launch_bounds__(NT, 1) void gemm256_kernel(Args p) {
     uint32_t toff = 0, boff = kt * (BK * 2);
     int tap = 0;
     if constexpr (AMODE == 3) {
-      tap = kt / csteps;
+      tap = cpow2 ? kt >> cshift : kt / csteps;
       const int c0 = (kt - tap * csteps) * BK;
-      const int tr = tap / p.ks, ts = tap - tr * p.ks;
+      const int tr = p.ks == 3 ? (tap * 11) >> 5 : tap / p.ks;     // tap < 9: (11 t) >> 5 = t / 3
+      const int ts = tap - tr * p.ks;
       toff = (uint32_t)(((tr * p.W + ts) * p.Cin + c0) * 2);
     }
     if constexpr (AMODE == 4) {
       // class tap t: row tap r' = ph ? 2 tR : 1 (dy row + tR), column s' = pw ? 2 tS : 1
-      const int t = kt / csteps;
+      const int t = cpow2 ? kt >> cshift : kt / csteps;
       const int c0 = (kt - t * csteps) * BK;
       const int tR = p.pw ? t >> 1 : t, tS = p.pw ? t & 1 : 0;
       const int rr = p.ph ? 2 * tR : 1, ss = p.pw ? 2 * tS : 1;
