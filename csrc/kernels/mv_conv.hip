@@ -166,6 +166,9 @@ __attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void con
   const int n0 = nt * BN;
   const int taps = g.ks * g.ks;
   const int csteps = g.C / BK, KT = (DG ? (1 + g.ph) * (1 + g.pw) : taps) * csteps;
+  // (tap, channel step) of a K tile by shift for power-of-two steps (C = 64 / 128 / 256 ..)
+  const bool cpow2 = (csteps & (csteps - 1)) == 0;
+  const int cshift = __builtin_ctz((unsigned)csteps);
   const int64_t wrow = (int64_t)taps * g.C;       // filter row length
   const int sc = (tid & 7) ^ ((tid >> 3) & 7);    // swizzled source chunk of this thread
 
@@ -176,7 +179,7 @@ __attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void con
   const uint64_t zaddr = (uint64_t)(g_zero + (tid & 7) * 4);
 
   auto issue = [&](const RowInfo<A_CH>& ri, int kt, int buf) {
-    int tap = kt / csteps;
+    int tap = cpow2 ? kt >> cshift : kt / csteps;
     const int c0 = (kt - tap * csteps) * BK;   // wave-uniform
     int64_t offa, offb;
     if constexpr (DG) {
@@ -187,7 +190,8 @@ __attribute__((amdgpu_waves_per_eu((NS == 2 && WM * WN == 8) ? 4 : 1))) void con
       offb = ((int64_t)(rr * 3 + ss) * g.C + c0) * 2;
       tap = 2 * tR + tS;                     // validity bit
     } else {
-      const int r = tap / g.ks, s = tap - r * g.ks;
+      const int r = g.ks == 3 ? (tap * 11) >> 5 : tap / g.ks;     // tap < 9: (11 t) >> 5 = t / 3
+      const int s = tap - r * g.ks;
       offa = (((int64_t)r * g.W + s) * g.C + c0) * 2;
       offb = ((int64_t)tap * g.C + c0) * 2;
     }
